@@ -1,0 +1,261 @@
+#!/usr/bin/env python
+"""Benchmark of the drone step path: env-steps/s per node, HBM roofline, CPU baseline.
+
+    python bench.py [--gpus N --steps K --warmup W]                      # 1 GPU
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N  # N GPUs
+
+A "step" is one frame of every drone on every rank: one ``dd_step`` launch
+per GPU over its resident shard (state, actions and outputs already in HBM).
+Default workload = BASELINE config 3 per GPU — 262,144 drones, randomised
+spawn, auto-reset, uniform random 3-bit actions, the [N,15] observation
+written every frame — so N=8 is config 4 (2,097,152 drones, weak scaling).
+Steps are replayed from a hipGraph (torch.cuda.CUDAGraph) of ``--graph-steps``
+launches; K steps are timed between barriers + device syncs, the max over
+ranks is reported.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import multiprocessing as mp
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "reinforcement-learning-101_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "env-steps/sec (whole node), N parallel drones, 1/2/4/8 MI355X; HBM GB/s %peak"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--envs-per-gpu", type=int, default=262_144)
+    p.add_argument("--precision", choices=("f32", "f64"), default="f32")
+    p.add_argument("--graph-steps", type=int, default=50, help="launches per captured hipGraph (0 = eager)")
+    p.add_argument("--no-obs", action="store_true", help="skip the observation write (not the default)")
+    p.add_argument("--action-rows", type=int, default=64, help="distinct pre-generated action rows cycled")
+    p.add_argument("--cpu-baseline", type=float, default=10.0, help="seconds of CPU-baseline wall time (0 = skip)")
+    p.add_argument("--cpu-workers", type=int, default=0, help="CPU-baseline processes (0 = min(16, cpus))")
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args()
+
+
+# ----------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    lane0, lanes, steps, seed = args
+    from delivery_drone_amd.config import EnvConfig
+    from oracle import oracle as ora
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    t0 = time.perf_counter()
+    chk = ora.bench(cfg, lane0, lanes, steps)
+    return time.perf_counter() - t0, chk
+
+
+def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
+    """The fixture-pinned C restatement of DroneGame.step (oracle/) on the
+    host's cores, config-3 workload (random spawn, auto-reset, random actions,
+    obs built every frame), a bounded sample sized to ~`seconds` of wall."""
+    from oracle import oracle as ora
+    ora.build()
+    lanes = 16_384
+    calib_steps = 20
+    dt, _ = _cpu_worker((0, lanes, calib_steps, seed))
+    per_lane_step = dt / (lanes * calib_steps)
+    steps = max(1, int(seconds / (per_lane_step * lanes)))
+    ctx = mp.get_context("fork")  # before any GPU call in this process
+    jobs = [(w * lanes, lanes, steps, seed) for w in range(workers)]
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    total = workers * lanes * steps
+    if not all(math.isfinite(c) for _, c in res):
+        raise RuntimeError("CPU baseline produced a non-finite checksum")
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except (OSError, IndexError):
+        model = platform.processor()
+    return {
+        "value": total / wall,
+        "unit": "env-steps/s",
+        "cores": workers,
+        "kind": "port",
+        "sample": (f"oracle/drone_oracle.c (fixture-pinned scalar f64 restatement of DroneGame.step + "
+                   f"get_state), config-3 workload: {workers} processes x {lanes} drones x {steps} frames "
+                   f"= {total:.3g} drone-steps in {wall:.1f} s on {model}; single-process "
+                   f"{1.0 / per_lane_step:.3g} steps/s"),
+    }
+
+
+# ------------------------------------------------------------------- GPU bench
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
+        args.gpus = world
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline > 0:
+        workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(args.cpu_baseline, workers, args.seed)
+
+    import torch
+    import torch.distributed as dist
+
+    from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n = args.envs_per_gpu
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=args.seed)
+    env = VecDroneEnv(n, device=dev, config=cfg, precision=args.precision, env_id_base=rank * n)
+    env.reset()
+    gen = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
+    rows = torch.randint(0, 8, (args.action_rows, n), device=dev, generator=gen, dtype=torch.uint8)
+    write_obs = not args.no_obs
+
+    stream = torch.cuda.Stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))
+    counter = [0]
+
+    def one_step():
+        env.step(rows[counter[0] % args.action_rows], write_obs=write_obs)
+        counter[0] += 1
+
+    G = args.graph_steps
+    graph = None
+    with torch.cuda.stream(stream):
+        if G > 0:
+            for _ in range(3):  # settle allocations before capture
+                one_step()
+            torch.cuda.synchronize(dev)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                for i in range(G):
+                    env.step(rows[i % args.action_rows], write_obs=write_obs)
+            single = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(single, stream=stream):
+                env.step(rows[0], write_obs=write_obs)
+
+        def run(k: int):
+            if graph is None:
+                for _ in range(k):
+                    one_step()
+                return
+            for _ in range(k // G):
+                graph.replay()
+            for _ in range(k % G):
+                single.replay()
+
+        run(args.warmup)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        run(args.steps)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+
+    stats = torch.tensor([wall, gpu_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    wall, gpu_ms = float(stats[0]), float(stats[1])
+
+    # sanity: the batch is alive and finite
+    assert torch.isfinite(env.obs).all().item() and int(env.episode.max()) >= 1
+
+    if rank == 0:
+        total_steps = n * world * args.steps
+        value = total_steps / wall
+        step_ms = gpu_ms / args.steps  # device time per launch on the kernel's stream
+        bytes_env = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=write_obs)
+        achieved = bytes_env * n / (step_ms * 1e-3) / 1e9
+        roof = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic(n, args.precision, write_obs),
+            "bytes_per_env": bytes_env,
+            "kernel": "dd::step_kernel<float,0>" if args.precision == "f32" else "dd::step_kernel<double,0>",
+            "timing": "HIP events on the launch stream over the K timed steps / K",
+        }
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall * 1e3 / args.steps, 6),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: Philox4x32 random spawns, uniform random 3-bit actions from a device-resident ring",
+            "config": {
+                "workload": ("config3/config4: 262144 drones per GPU, randomised spawn + auto-reset; "
+                             "N GPUs = N x 262144 (config 4 at N=8)" if n == 262_144 else
+                             f"{n} drones per GPU, randomised spawn + auto-reset"),
+                "envs_per_gpu": n,
+                "global_envs": n * world,
+                "storage": args.precision,
+                "compute": "f64 (reference arithmetic, rounded once on store)",
+                "obs": "[N,15] f32 every step" if write_obs else "off",
+                "actions": "u8 bitmask [N]",
+                "launch": f"hipGraph of {G} steps" if G > 0 else "eager",
+                "parallelism": f"env-shard x{world} (no collective on the step path)",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "gpu_ms_per_step": round(step_ms, 6),
+            "device": torch.cuda.get_device_name(dev),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def pmc_traffic(n: int, precision: str, obs: bool):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, produced by tools/profile.sh), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for r in rows.get("rows", []):
+        if r.get("envs") == n and r.get("precision") == precision and r.get("obs") == obs:
+            return r.get("hbm_bytes_per_launch")
+    return None
+
+
+if __name__ == "__main__":
+    main()

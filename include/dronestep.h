@@ -1,0 +1,198 @@
+/*
+ * dronestep.h — C-ABI of the MI355X-native vectorised delivery-drone step.
+ *
+ * This is the drop-in boundary for the reference's per-frame hot path
+ * (vedant-jumle/reinforcement-learning-101, delivery_drone/game/):
+ *
+ *   DroneGame.step     game_engine.py:95-138   -> dd_step
+ *   DroneGame.reset    game_engine.py:59-93    -> dd_reset
+ *   DroneGame.get_state game_engine.py:140-177 -> dd_write_obs
+ *   DroneGame._get_info game_engine.py:281-298 -> dd_get_info
+ *   config.py:17-68 module constants           -> DDConfig (dd_config_default)
+ *
+ * One call processes a batch of N independent drones stored as a
+ * struct-of-arrays (SoA) in device memory.  The reference has no FFI of its
+ * own (it is 100 % Python and its only cross-process surface is the JSON
+ * socket protocol of game/socket_server.py:126-263); these entry points are
+ * what a ctypes / cffi binding of that path binds.
+ *
+ * Conventions
+ *  - The caller owns every buffer.  Nothing here allocates, frees or keeps a
+ *    pointer past the call.  All work is enqueued on `stream` (a hipStream_t
+ *    passed as void*; NULL = the legacy default stream) and is asynchronous.
+ *  - Return value: 0 on success, otherwise a hipError_t code
+ *    (1 = hipErrorInvalidValue for argument errors).  No exceptions cross the
+ *    ABI.  dd_error_string() turns a code into text.
+ *  - Floating-point fields are either all float (DD_F32) or all double
+ *    (DD_F64); the arithmetic is always IEEE double, matching the reference's
+ *    Python floats, and results are rounded once on store.
+ */
+#ifndef DRONESTEP_H
+#define DRONESTEP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DD_ABI_VERSION 1
+
+/* Storage precision of the SoA floating-point fields. */
+enum { DD_F32 = 0, DD_F64 = 1 };
+
+/* Action encodings accepted by dd_step (DDStepIO.action_format).
+ * The reference takes a dict {main_thrust, left_thrust, right_thrust} and
+ * casts each with bool() (game_engine.py:114-118). */
+enum {
+    DD_ACT_BITMASK = 0, /* uint8[N], bit0 = main, bit1 = left, bit2 = right  */
+    DD_ACT_F32X3 = 1,   /* float[N][3] (main, left, right), nonzero = on;     */
+                        /* the notebooks' Bernoulli(probs).sample() layout     */
+    DD_ACT_U8X3 = 2     /* uint8/bool[N][3] (main, left, right), nonzero = on */
+};
+
+/* Status byte bits (DDState.status). */
+enum {
+    DD_ST_DONE = 1u << 0,    /* DroneGame.done                    */
+    DD_ST_LANDED = 1u << 1,  /* Drone.landed                      */
+    DD_ST_CRASHED = 1u << 2, /* Drone.crashed                     */
+    DD_ST_PLAT_LEFT = 1u << 3 /* Platform.direction == -1 (moving) */
+};
+
+/* Width of one observation row: state_to_array order of
+ * Actor_Critic_PPO.ipynb:346-366 (x, y, vx, vy, angle, omega, fuel, px, py,
+ * distance, dx, dy, speed, landed, crashed), each normalised exactly as
+ * DroneGame.get_state (game_engine.py:151-175). */
+#define DD_OBS_DIM 15
+
+/* World constants.  dd_config_default() fills the values of config.py. */
+typedef struct DDConfig {
+    /* physics — config.py:18-29, drone.py:44-103 */
+    double gravity;           /* GRAVITY 0.3                  */
+    double drag;              /* DRAG 0.99                    */
+    double angular_drag;      /* ANGULAR_DRAG 0.95            */
+    double main_thrust_power; /* MAIN_THRUST_POWER 0.6        */
+    double side_thrust_power; /* SIDE_THRUST_POWER 0.3        */
+    double fuel_main;         /* FUEL_CONSUMPTION_MAIN 2.0    */
+    double fuel_side;         /* FUEL_CONSUMPTION_SIDE 1.0    */
+    double max_fuel;          /* MAX_FUEL 1000.0              */
+    double drone_half_height; /* DRONE_HEIGHT / 2 = 10.0 (get_bottom_center) */
+    double dt;                /* update(dt=1.0)               */
+    /* platform — config.py:32-36, platform.py:11-62 */
+    double platform_half_width;  /* PLATFORM_WIDTH / 2 = 50.0  */
+    double platform_half_height; /* PLATFORM_HEIGHT / 2 = 10.0 */
+    double platform_speed;       /* PLATFORM_SPEED 1.0         */
+    double platform_min_x;       /* width // 2 = 50            */
+    double platform_max_x;       /* WINDOW_WIDTH - width // 2 = 750 */
+    /* landing — config.py:39-40 */
+    double max_landing_velocity; /* 3.0  */
+    double max_landing_angle;    /* 20.0 */
+    /* bounds — config.py:3-4, 45; game_engine.py:254 */
+    double world_width;  /* 800 */
+    double world_height; /* 600 */
+    double oob_margin;   /* 50  */
+    double ground_level; /* WINDOW_HEIGHT - 50 = 550 */
+    /* wind — config.py:48-49, game_engine.py:121-123 */
+    double wind_x, wind_y;
+    /* rewards — config.py:54-58, game_engine.py:185-214 */
+    double reward_step;          /* -0.1   */
+    double reward_landing;       /* 100.0  */
+    double reward_crash;         /* -100.0 */
+    double reward_out_of_fuel;   /* -50.0  */
+    double reward_out_of_bounds; /* -50.0  */
+    double shaping_offset;       /* 500  in (500 - dist) / 5000 */
+    double shaping_scale;        /* 5000 */
+    /* observation scales — game_engine.py:155-171 */
+    double vel_scale;   /* 10.0  */
+    double angle_scale; /* 180.0 */
+    /* spawn — config.py:61-68, game_engine.py:66-85 (integer ranges) */
+    int32_t drone_start_x, drone_start_y;         /* fixed spawn 400, 100 */
+    int32_t drone_x_min, drone_x_max;             /* inclusive 100..700   */
+    int32_t drone_y_min, drone_y_max;             /* inclusive 50..250    */
+    int32_t platform_start_x, platform_start_y;   /* fixed 400, 500       */
+    int32_t platform_x_lo, platform_x_hi;         /* half-open [100, 700) */
+    int32_t platform_y_lo, platform_y_hi;         /* half-open [100, 550) */
+    /* switches */
+    int32_t wind_enabled;       /* WIND_ENABLED False      */
+    int32_t platform_moving;    /* PLATFORM_MOVING False   */
+    int32_t randomize_drone;    /* DroneGame(randomize_drone=False)   */
+    int32_t randomize_platform; /* DroneGame(randomize_platform=True) */
+    int32_t auto_reset;         /* 0: sticky done (game_engine.py:107-111);
+                                   1: a lane that is done when dd_step starts is
+                                   re-spawned and returns its reset observation
+                                   with reward 0 and done 0 (next-step reset). */
+    int32_t _pad;
+    uint64_t seed; /* Philox4x32-10 key for spawn draws */
+} DDConfig;
+
+/* The SoA.  Every pointer addresses N elements in device memory.  The eleven
+ * floating-point arrays are float* (DD_F32) or double* (DD_F64). */
+typedef struct DDState {
+    void *x, *y, *vx, *vy, *angle, *omega, *fuel; /* Drone: drone.py:19-33      */
+    void *px, *py;                                /* Platform.x / .y            */
+    void *total_reward;                           /* DroneGame.total_reward     */
+    uint8_t *status;                              /* DD_ST_* bits               */
+    int32_t *steps;                               /* DroneGame.steps            */
+    int32_t *episode;                             /* DroneGame.episode          */
+    int64_t env_id_base; /* global id of element 0 (sharding-invariant RNG)    */
+    int32_t precision;   /* DD_F32 or DD_F64                                   */
+    int32_t _pad;
+} DDState;
+
+/* Per-call inputs and outputs of dd_step. */
+typedef struct DDStepIO {
+    const void *actions;  /* see action_format (required)                      */
+    int32_t action_format;
+    int32_t _pad;
+    void *reward;         /* float or double [N] by precision (required)        */
+    uint8_t *done;        /* uint8 [N], 1 = done after this call (required)     */
+    float *obs;           /* float [N][15] (nullable)                           */
+    int32_t *done_idx;    /* lanes whose episode ended in this call, in any
+                             order (nullable; wave-ballot compaction)            */
+    int32_t *done_count;  /* number of entries written to done_idx (zeroed by
+                             dd_step; required iff done_idx != NULL)             */
+} DDStepIO;
+
+/* Fills *cfg with config.py's values (randomize_platform = 1, others 0). */
+void dd_config_default(DDConfig *cfg);
+
+/* One frame for every lane: DroneGame.step (game_engine.py:95-138). */
+int dd_step(const DDConfig *cfg, const DDState *st, const DDStepIO *io,
+            int64_t n, void *stream);
+
+/* Re-spawn lanes (DroneGame.reset, game_engine.py:59-93).  mask: uint8 [N],
+ * nonzero = reset that lane; NULL = all lanes.  obs (nullable) receives the
+ * reset observation of the reset lanes; other rows are left untouched. */
+int dd_reset(const DDConfig *cfg, const DDState *st, const uint8_t *mask,
+             float *obs, int64_t n, void *stream);
+
+/* Observation rows from the current state (DroneGame.get_state). */
+int dd_write_obs(const DDConfig *cfg, const DDState *st, float *obs,
+                 int64_t n, void *stream);
+
+/* Pixel-unit distance to the platform and speed (DroneGame._get_info,
+ * game_engine.py:292-296); float or double [N] by precision. */
+int dd_get_info(const DDConfig *cfg, const DDState *st, void *distance,
+                void *speed, int64_t n, void *stream);
+
+/* Ordered compaction: idx_out receives, in ascending order, every i with
+ * (flags[i] != 0) == (want != 0); *count its length.  Builds the notebooks'
+ * active-game list (Actor_Critic_PPO.ipynb:840-850) on device.
+ * workspace: int32 [dd_compact_workspace(n)] scratch. */
+int64_t dd_compact_workspace(int64_t n);
+int dd_compact(const uint8_t *flags, int32_t want, int32_t *idx_out,
+               int32_t *count, int32_t *workspace, int64_t n, void *stream);
+
+/* Algorithmic HBM bytes of one dd_step lane (the roofline byte model,
+ * DESIGN.md §4): precision, action format, obs on/off. */
+int64_t dd_step_bytes_per_env(int32_t precision, int32_t action_format,
+                              int32_t with_obs);
+
+const char *dd_error_string(int code);
+int dd_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DRONESTEP_H */

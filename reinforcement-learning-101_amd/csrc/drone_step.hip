@@ -1,0 +1,695 @@
+// drone_step.hip — MI355X (gfx950) kernels behind include/dronestep.h.
+//
+// One lane = one drone.  The frame of DroneGame.step (reference
+// delivery_drone/game/game_engine.py:95-138) is evaluated in IEEE double in
+// registers, in the reference's operation order, and rounded once on store
+// (DD_F32) or not at all (DD_F64).  The path is HBM-bound (~1 flop/B), so the
+// kernel is shaped for bytes, not FLOPs: SoA dword loads/stores coalesced per
+// wave64, world constants in the kernarg segment (SGPRs, wave-uniform),
+// observation rows transposed through LDS so the [N,15] tile leaves as
+// contiguous 16-byte stores, and done-lane compaction by wave ballots with one
+// atomic per wave.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
+// (-ffp-contract=off keeps every a*b+c as the reference's two roundings.)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dronestep.h"
+
+namespace dd {
+
+constexpr int kBlock = 256;  // 4 waves; one obs tile = 256 rows
+constexpr int kWave = 64;
+
+// numpy's deg2rad: x * (NPY_PI / 180.0)   (physics.py:16, np.radians)
+constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11).  Spawn draws are keyed by
+// (seed; global env id, episode) so a lane's spawn is independent of how the
+// batch is sharded across ranks and of the launch geometry.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
+                                              uint32_t c3, uint32_t k0, uint32_t k1,
+                                              uint32_t out[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// Uniform integer in [lo, lo + span) from one 32-bit draw (multiply-high).
+__device__ __forceinline__ int32_t draw_range(uint32_t r, int32_t lo, uint32_t span) {
+    return lo + (int32_t)(((uint64_t)r * span) >> 32);
+}
+
+// World constants as the kernels see them: the public config plus the
+// correctly rounded reciprocals of the divisors, computed once on the host.
+struct Consts {
+    DDConfig c;
+    double inv_w, inv_h, inv_vel, inv_angle, inv_fuel, inv_shaping;
+};
+
+inline Consts make_consts(const DDConfig& c) {
+    Consts k;
+    k.c = c;
+    k.inv_w = 1.0 / c.world_width;
+    k.inv_h = 1.0 / c.world_height;
+    k.inv_vel = 1.0 / c.vel_scale;
+    k.inv_angle = 1.0 / c.angle_scale;
+    k.inv_fuel = 1.0 / c.max_fuel;
+    k.inv_shaping = 1.0 / c.shaping_scale;
+    return k;
+}
+
+// x / d, correctly rounded, in three double ops instead of the ~10 of the
+// general division sequence.  inv_d = RN(1/d); q0 = RN(x * inv_d) is faithful,
+// so by Markstein's theorem RN(q0 + RN(1/d) * (x - q0 * d)) = RN(x / d), the
+// reference's quotient, bit for bit (finite operands, no underflow).
+__device__ __forceinline__ double div_exact(double x, double d, double inv_d) {
+    const double q0 = x * inv_d;
+    const double r = fma(-q0, d, x);
+    return fma(r, inv_d, q0);
+}
+
+// The per-lane state, widened to double for the frame's arithmetic.
+struct Lane {
+    double x, y, vx, vy, angle, omega, fuel, px, py, total;
+    uint32_t status;
+    int32_t steps, episode;
+};
+
+// DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
+// Platform.reset (platform.py:104-114).  `episode` is the value after the
+// reset's `episode += 1`.
+__device__ __forceinline__ void spawn(const DDConfig& c, int64_t env, Lane& s) {
+    s.episode += 1;
+    uint32_t r[4];
+    philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)s.episode, 0u,
+                  (uint32_t)c.seed, (uint32_t)(c.seed >> 32), r);
+    if (c.randomize_drone) {
+        s.x = draw_range(r[0], c.drone_x_min, (uint32_t)(c.drone_x_max - c.drone_x_min + 1));
+        s.y = draw_range(r[1], c.drone_y_min, (uint32_t)(c.drone_y_max - c.drone_y_min + 1));
+    } else {
+        s.x = c.drone_start_x;
+        s.y = c.drone_start_y;
+    }
+    if (c.randomize_platform) {
+        s.px = draw_range(r[2], c.platform_x_lo, (uint32_t)(c.platform_x_hi - c.platform_x_lo));
+        s.py = draw_range(r[3], c.platform_y_lo, (uint32_t)(c.platform_y_hi - c.platform_y_lo));
+    } else {
+        s.px = c.platform_start_x;
+        s.py = c.platform_start_y;
+    }
+    s.vx = 0.0; s.vy = 0.0; s.angle = 0.0; s.omega = 0.0;
+    s.fuel = c.max_fuel;
+    s.status = 0u;  // not done / landed / crashed; platform direction +1
+    s.steps = 0;
+    s.total = 0.0;
+}
+
+// physics.normalize_angle (physics.py:26-39).  From any state step() can
+// reach, |omega| < 6 deg/frame, so the loops run at most once; the guard keeps
+// every wave finite for an arbitrary user-written angle.
+__device__ __forceinline__ double normalize_angle(double a) {
+    int guard = 0;
+    while (a > 180.0 && guard < 64) { a -= 360.0; ++guard; }
+    while (a < -180.0 && guard < 128) { a += 360.0; ++guard; }
+    return a;
+}
+
+// One frame of a live lane: Drone.apply_thrust (drone.py:44-76), wind
+// (game_engine.py:121-123), Drone.update (drone.py:78-103), Platform.update
+// (platform.py:31-49), _calculate_reward with _check_landing / _check_crash /
+// _check_out_of_bounds (game_engine.py:179-279).  Returns the reward.
+__device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) {
+    const DDConfig& c = k.c;
+    const bool main_on = act & 1u, left_on = act & 2u, right_on = act & 4u;
+
+    if (main_on && s.fuel > 0.0) {
+        // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
+        double sa, ca;
+        sincos(s.angle * kDeg2Rad, &sa, &ca);
+        const double ty = -c.main_thrust_power;
+        s.vx += 0.0 * ca - ty * sa;
+        s.vy += 0.0 * sa + ty * ca;
+        s.fuel -= c.fuel_main;
+    }
+    if (left_on && s.fuel > 0.0) { s.omega -= c.side_thrust_power; s.fuel -= c.fuel_side; }
+    if (right_on && s.fuel > 0.0) { s.omega += c.side_thrust_power; s.fuel -= c.fuel_side; }
+    s.fuel = s.fuel > 0.0 ? s.fuel : 0.0;  // max(0, fuel)
+
+    if (c.wind_enabled) { s.vx += c.wind_x; s.vy += c.wind_y; }
+
+    s.vy += c.gravity * c.dt;
+    s.vx *= c.drag;
+    s.vy *= c.drag;
+    s.x += s.vx * c.dt;
+    s.y += s.vy * c.dt;
+    s.angle += s.omega * c.dt;
+    s.omega *= c.angular_drag;
+    s.angle = normalize_angle(s.angle);
+
+    if (c.platform_moving) {
+        const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
+        s.px += c.platform_speed * dir * c.dt;
+        if (s.px <= c.platform_min_x) { s.px = c.platform_min_x; s.status &= ~DD_ST_PLAT_LEFT; }
+        else if (s.px >= c.platform_max_x) { s.px = c.platform_max_x; s.status |= DD_ST_PLAT_LEFT; }
+    }
+
+    // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
+    double sb, cb;
+    sincos(s.angle * kDeg2Rad, &sb, &cb);
+    const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
+    const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
+    const bool on_pad = (s.px - c.platform_half_width <= bx) && (bx <= s.px + c.platform_half_width) &&
+                        (s.py - c.platform_half_height <= by) && (by <= s.py + c.platform_half_height);
+    const double speed = sqrt(s.vx * s.vx + s.vy * s.vy);
+    const bool slow = !(speed > c.max_landing_velocity);
+    const bool upright = fabs(s.angle) <= c.max_landing_angle;
+
+    double reward = c.reward_step;
+    if (on_pad && slow && upright) {                      // _check_landing
+        s.status |= DD_ST_LANDED | DD_ST_DONE;
+        reward += c.reward_landing;
+    } else if (s.y > c.ground_level) {                    // _check_crash (landing ruled out)
+        s.status |= DD_ST_CRASHED | DD_ST_DONE;
+        reward += c.reward_crash;
+    } else if (s.fuel <= 0.0) {                           // out of fuel
+        s.status |= DD_ST_CRASHED | DD_ST_DONE;
+        reward += c.reward_out_of_fuel;
+    } else if (s.x < -c.oob_margin || s.x > c.world_width + c.oob_margin ||
+               s.y < -c.oob_margin || s.y > c.world_height + c.oob_margin) {
+        s.status |= DD_ST_CRASHED | DD_ST_DONE;
+        reward += c.reward_out_of_bounds;
+    } else {                                              // proximity shaping
+        const double dx = s.px - s.x, dy = s.py - s.y;
+        const double dist = sqrt(dx * dx + dy * dy);
+        reward += div_exact(c.shaping_offset - dist, c.shaping_scale, k.inv_shaping);
+    }
+    s.total += reward;
+    s.steps += 1;
+    return reward;
+}
+
+// DroneGame.get_state (game_engine.py:140-177) in state_to_array order.
+__device__ __forceinline__ void observe(const Consts& k, const Lane& s, float o[DD_OBS_DIM]) {
+    const DDConfig& c = k.c;
+    const double dx = s.px - s.x, dy = s.py - s.y;
+    const double dist = sqrt(dx * dx + dy * dy);
+    const double speed = sqrt(s.vx * s.vx + s.vy * s.vy);
+    o[0] = (float)div_exact(s.x, c.world_width, k.inv_w);
+    o[1] = (float)div_exact(s.y, c.world_height, k.inv_h);
+    o[2] = (float)div_exact(s.vx, c.vel_scale, k.inv_vel);
+    o[3] = (float)div_exact(s.vy, c.vel_scale, k.inv_vel);
+    o[4] = (float)div_exact(s.angle, c.angle_scale, k.inv_angle);
+    o[5] = (float)div_exact(s.omega, c.vel_scale, k.inv_vel);
+    o[6] = (float)div_exact(s.fuel, c.max_fuel, k.inv_fuel);
+    o[7] = (float)div_exact(s.px, c.world_width, k.inv_w);
+    o[8] = (float)div_exact(s.py, c.world_height, k.inv_h);
+    o[9] = (float)div_exact(dist, c.world_width, k.inv_w);
+    o[10] = (float)div_exact(dx, c.world_width, k.inv_w);
+    o[11] = (float)div_exact(dy, c.world_height, k.inv_h);
+    o[12] = (float)div_exact(speed, c.vel_scale, k.inv_vel);
+    o[13] = (s.status & DD_ST_LANDED) ? 1.0f : 0.0f;
+    o[14] = (s.status & DD_ST_CRASHED) ? 1.0f : 0.0f;
+}
+
+template <typename T>
+struct Soa {
+    T *x, *y, *vx, *vy, *angle, *omega, *fuel, *px, *py, *total;
+    uint8_t* status;
+    int32_t *steps, *episode;
+    int64_t env_id_base;
+};
+
+template <typename T>
+__host__ Soa<T> soa_of(const DDState& st) {
+    Soa<T> s;
+    s.x = (T*)st.x; s.y = (T*)st.y; s.vx = (T*)st.vx; s.vy = (T*)st.vy;
+    s.angle = (T*)st.angle; s.omega = (T*)st.omega; s.fuel = (T*)st.fuel;
+    s.px = (T*)st.px; s.py = (T*)st.py; s.total = (T*)st.total_reward;
+    s.status = st.status; s.steps = st.steps; s.episode = st.episode;
+    s.env_id_base = st.env_id_base;
+    return s;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_dynamics(const Soa<T>& a, int64_t i, Lane& s) {
+    s.x = a.x[i]; s.y = a.y[i]; s.vx = a.vx[i]; s.vy = a.vy[i];
+    s.angle = a.angle[i]; s.omega = a.omega[i]; s.fuel = a.fuel[i];
+    s.px = a.px[i]; s.py = a.py[i];
+}
+
+template <typename T>
+__device__ __forceinline__ void store_dynamics(const Soa<T>& a, int64_t i, const Lane& s) {
+    a.x[i] = (T)s.x; a.y[i] = (T)s.y; a.vx[i] = (T)s.vx; a.vy[i] = (T)s.vy;
+    a.angle[i] = (T)s.angle; a.omega[i] = (T)s.omega; a.fuel[i] = (T)s.fuel;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_spawn(const Soa<T>& a, int64_t i, const Lane& s) {
+    store_dynamics(a, i, s);
+    a.px[i] = (T)s.px; a.py[i] = (T)s.py;
+    a.total[i] = (T)s.total;
+    a.status[i] = (uint8_t)s.status;
+    a.steps[i] = s.steps;
+    a.episode[i] = s.episode;
+}
+
+// Writes the block's [rows, 15] observation tile from LDS to global memory as
+// 16-byte stores.  `tile` holds rows * 15 floats; obs_row0 = first row.
+__device__ __forceinline__ void flush_obs_tile(const float* tile, float* obs, int64_t row0, int rows) {
+    float* dst = obs + row0 * DD_OBS_DIM;
+    const int nf = rows * DD_OBS_DIM;
+    // row0 is a multiple of kBlock, so dst is 16-byte aligned whenever obs is.
+    const bool aligned = ((uintptr_t)dst & 15u) == 0;
+    if (aligned) {
+        const int nv = nf >> 2;
+        const float4* src4 = reinterpret_cast<const float4*>(tile);
+        float4* dst4 = reinterpret_cast<float4*>(dst);
+        for (int k = threadIdx.x; k < nv; k += kBlock) dst4[k] = src4[k];
+        for (int k = (nv << 2) + threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
+    } else {
+        for (int k = threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
+    }
+}
+
+struct StepArgs {
+    Consts k;
+    const void* actions;
+    void* reward;
+    uint8_t* done;
+    float* obs;
+    int32_t* done_idx;
+    int32_t* done_count;
+    int64_t n;
+};
+
+template <int AFMT>
+__device__ __forceinline__ uint32_t load_action(const void* actions, int64_t i) {
+    if constexpr (AFMT == DD_ACT_BITMASK) {
+        return static_cast<const uint8_t*>(actions)[i];
+    } else if constexpr (AFMT == DD_ACT_F32X3) {
+        const float* a = static_cast<const float*>(actions) + 3 * i;
+        return (a[0] != 0.0f ? 1u : 0u) | (a[1] != 0.0f ? 2u : 0u) | (a[2] != 0.0f ? 4u : 0u);
+    } else {
+        const uint8_t* a = static_cast<const uint8_t*>(actions) + 3 * i;
+        return (a[0] ? 1u : 0u) | (a[1] ? 2u : 0u) | (a[2] ? 4u : 0u);
+    }
+}
+
+// dd_step kernel.  One 256-lane tile per block.  (A grid-stride loop makes
+// hipcc hoist every kernarg constant out of the loop: 147 SGPR spills and 137
+// VGPRs against 0 and 74 for one tile per block.)
+template <typename T, int AFMT>
+__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs p, Soa<T> a) {
+    __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
+    const DDConfig& c = p.k.c;
+    {
+        const int64_t t = blockIdx.x;
+        const int64_t i = t * kBlock + threadIdx.x;
+        const bool live = i < p.n;
+        bool ended = false;  // episode ended in this call (for compaction)
+        Lane s;
+        float o[DD_OBS_DIM];
+        if (live) {
+            load_dynamics(a, i, s);
+            s.status = a.status[i];
+            s.steps = a.steps[i];
+            s.total = a.total[i];
+            const uint32_t act = load_action<AFMT>(p.actions, i);
+            double reward;
+            if (s.status & DD_ST_DONE) {
+                reward = 0.0;
+                if (c.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
+                    s.episode = a.episode[i];
+                    spawn(c, a.env_id_base + i, s);
+                    store_spawn(a, i, s);
+                } // else sticky done (game_engine.py:107-111): nothing changes
+            } else {
+                reward = frame(p.k, act, s);
+                ended = (s.status & DD_ST_DONE) != 0;
+                store_dynamics(a, i, s);
+                if (c.platform_moving) { a.px[i] = (T)s.px; a.status[i] = (uint8_t)s.status; }
+                else if (ended) a.status[i] = (uint8_t)s.status;
+                a.steps[i] = s.steps;
+                a.total[i] = (T)s.total;
+            }
+            static_cast<T*>(p.reward)[i] = (T)reward;
+            p.done[i] = (s.status & DD_ST_DONE) ? 1 : 0;
+            if (p.obs) observe(p.k, s, o);
+        }
+        if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
+            const uint64_t m = __ballot(ended);
+            if (m) {
+                const int lane = threadIdx.x & (kWave - 1);
+                const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                int base = 0;
+                if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(p.done_count, __popcll(m));
+                base = __shfl(base, __ffsll((unsigned long long)m) - 1);
+                if (ended) p.done_idx[base + before] = (int32_t)i;
+            }
+        }
+        if (p.obs) {  // uniform across the grid
+            if (live) {
+#pragma unroll
+                for (int k = 0; k < DD_OBS_DIM; ++k) tile[threadIdx.x * DD_OBS_DIM + k] = o[k];
+            }
+            __syncthreads();
+            const int64_t row0 = t * kBlock;
+            const int rows = (int)((p.n - row0) < kBlock ? (p.n - row0) : kBlock);
+            flush_obs_tile(tile, p.obs, row0, rows);
+            __syncthreads();
+        }
+    }
+}
+
+// dd_reset kernel: masked re-spawn (+ optional reset observation).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void reset_kernel(Consts k, Soa<T> a, const uint8_t* mask,
+                                                       float* obs, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (mask && !mask[i]) return;
+    Lane s;
+    s.episode = a.episode[i];
+    spawn(k.c, a.env_id_base + i, s);
+    store_spawn(a, i, s);
+    if (obs) {
+        float o[DD_OBS_DIM];
+        observe(k, s, o);
+        float* row = obs + i * DD_OBS_DIM;
+#pragma unroll
+        for (int k = 0; k < DD_OBS_DIM; ++k) row[k] = o[k];
+    }
+}
+
+// dd_write_obs kernel: observation of the current state, LDS-staged.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void obs_kernel(Consts k, Soa<T> a, float* obs, int64_t n) {
+    __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
+    {
+        const int64_t t = blockIdx.x;
+        const int64_t i = t * kBlock + threadIdx.x;
+        if (i < n) {
+            Lane s;
+            load_dynamics(a, i, s);
+            s.status = a.status[i];
+            float o[DD_OBS_DIM];
+            observe(k, s, o);
+#pragma unroll
+            for (int k = 0; k < DD_OBS_DIM; ++k) tile[threadIdx.x * DD_OBS_DIM + k] = o[k];
+        }
+        __syncthreads();
+        const int64_t row0 = t * kBlock;
+        const int rows = (int)((n - row0) < kBlock ? (n - row0) : kBlock);
+        flush_obs_tile(tile, obs, row0, rows);
+        __syncthreads();
+    }
+}
+
+// dd_get_info kernel: pixel distance and speed (game_engine.py:292-296).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void info_kernel(Soa<T> a, T* distance, T* speed, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const double x = a.x[i], y = a.y[i], vx = a.vx[i], vy = a.vy[i];
+    const double dx = (double)a.px[i] - x, dy = (double)a.py[i] - y;
+    if (distance) distance[i] = (T)sqrt(dx * dx + dy * dy);
+    if (speed) speed[i] = (T)sqrt(vx * vx + vy * vy);
+}
+
+// ---------------------------------------------------------------------------
+// Ordered compaction (dd_compact): count per tile -> exclusive scan of tile
+// counts -> scatter in lane order.  Ballots give each wave its count and each
+// lane its rank; LDS combines the block's four waves.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool want_flag(const uint8_t* flags, int32_t want, int64_t i, int64_t n) {
+    return i < n && ((flags[i] != 0) == (want != 0));
+}
+
+__global__ __launch_bounds__(kBlock) void compact_count_kernel(const uint8_t* flags, int32_t want,
+                                                               int32_t* tile_counts, int64_t n) {
+    __shared__ int wave_cnt[kBlock / kWave];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t m = __ballot(want_flag(flags, want, i, n));
+    if ((threadIdx.x & (kWave - 1)) == 0) wave_cnt[threadIdx.x / kWave] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int sum = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) sum += wave_cnt[w];
+        tile_counts[blockIdx.x] = sum;
+    }
+}
+
+// Single-block exclusive scan over `m` tile counts; total goes to *count.
+__global__ __launch_bounds__(1024) void compact_scan_kernel(int32_t* tile_counts, int64_t m, int32_t* count) {
+    __shared__ int32_t part[1024];
+    __shared__ int32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < m; base += 1024) {
+        const int64_t j = base + threadIdx.x;
+        const int32_t v = j < m ? tile_counts[j] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+            const int32_t add = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (j < m) tile_counts[j] = carry + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *count = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void compact_scatter_kernel(const uint8_t* flags, int32_t want,
+                                                                 const int32_t* tile_offsets,
+                                                                 int32_t* idx_out, int64_t n) {
+    __shared__ int wave_off[kBlock / kWave];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool keep = want_flag(flags, want, i, n);
+    const uint64_t m = __ballot(keep);
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) wave_off[w] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = tile_offsets[blockIdx.x];
+        for (int k = 0; k < kBlock / kWave; ++k) { const int c = wave_off[k]; wave_off[k] = run; run += c; }
+    }
+    __syncthreads();
+    if (keep) {
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        idx_out[wave_off[w] + rank] = (int32_t)i;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side: argument checks and launches.
+// ---------------------------------------------------------------------------
+inline int64_t tiles_of(int64_t n) { return (n + kBlock - 1) / kBlock; }
+
+inline unsigned grid_of(int64_t n) { return (unsigned)tiles_of(n); }
+
+bool state_ok(const DDState* st) {
+    return st && st->x && st->y && st->vx && st->vy && st->angle && st->omega && st->fuel && st->px &&
+           st->py && st->total_reward && st->status && st->steps && st->episode &&
+           (st->precision == DD_F32 || st->precision == DD_F64);
+}
+
+template <typename T, int AFMT>
+void launch_step(const StepArgs& p, const DDState& st, hipStream_t s) {
+    hipLaunchKernelGGL((step_kernel<T, AFMT>), dim3(grid_of(p.n)), dim3(kBlock), 0, s, p, soa_of<T>(st));
+}
+
+template <typename T>
+void launch_step_t(const StepArgs& p, int afmt, const DDState& st, hipStream_t s) {
+    switch (afmt) {
+        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK>(p, st, s); break;
+        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3>(p, st, s); break;
+        default: launch_step<T, DD_ACT_U8X3>(p, st, s); break;
+    }
+}
+
+int finish() {
+    const hipError_t e = hipGetLastError();
+    return (int)e;
+}
+
+}  // namespace dd
+
+extern "C" {
+
+void dd_config_default(DDConfig* c) {
+    if (!c) return;
+    *c = DDConfig{};
+    c->gravity = 0.3;
+    c->drag = 0.99;
+    c->angular_drag = 0.95;
+    c->main_thrust_power = 0.6;
+    c->side_thrust_power = 0.3;
+    c->fuel_main = 2.0;
+    c->fuel_side = 1.0;
+    c->max_fuel = 1000.0;
+    c->drone_half_height = 20 / 2.0;
+    c->dt = 1.0;
+    c->platform_half_width = 100 / 2.0;
+    c->platform_half_height = 20 / 2.0;
+    c->platform_speed = 1.0;
+    c->platform_min_x = 100 / 2;
+    c->platform_max_x = 800 - 100 / 2;
+    c->max_landing_velocity = 3.0;
+    c->max_landing_angle = 20.0;
+    c->world_width = 800;
+    c->world_height = 600;
+    c->oob_margin = 50;
+    c->ground_level = 600 - 50;
+    c->wind_x = 0.0;
+    c->wind_y = 0.0;
+    c->reward_step = -0.1;
+    c->reward_landing = 100.0;
+    c->reward_crash = -100.0;
+    c->reward_out_of_fuel = -50.0;
+    c->reward_out_of_bounds = -50.0;
+    c->shaping_offset = 500;
+    c->shaping_scale = 5000;
+    c->vel_scale = 10.0;
+    c->angle_scale = 180.0;
+    c->drone_start_x = 800 / 2;
+    c->drone_start_y = 100;
+    c->drone_x_min = 100;
+    c->drone_x_max = 700;
+    c->drone_y_min = 50;
+    c->drone_y_max = 250;
+    c->platform_start_x = 800 / 2;
+    c->platform_start_y = 600 - 100;
+    c->platform_x_lo = 100 / 2 + 50;
+    c->platform_x_hi = 800 - 100 / 2 - 50;
+    c->platform_y_lo = 100;
+    c->platform_y_hi = 550;
+    c->wind_enabled = 0;
+    c->platform_moving = 0;
+    c->randomize_drone = 0;
+    c->randomize_platform = 1;
+    c->auto_reset = 0;
+    c->seed = 0;
+}
+
+int dd_step(const DDConfig* cfg, const DDState* st, const DDStepIO* io, int64_t n, void* stream) {
+    if (!cfg || !io || !st || n < 0 || n > INT32_MAX) return hipErrorInvalidValue;
+    if (io->action_format < DD_ACT_BITMASK || io->action_format > DD_ACT_U8X3) return hipErrorInvalidValue;
+    if (st->precision != DD_F32 && st->precision != DD_F64) return hipErrorInvalidValue;
+    if (io->done_idx && !io->done_count) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (io->done_count) {
+        const hipError_t e = hipMemsetAsync(io->done_count, 0, sizeof(int32_t), s);
+        if (e != hipSuccess) return (int)e;
+    }
+    if (n == 0) return 0;  // empty batch: pointers may be null
+    if (!dd::state_ok(st) || !io->actions || !io->reward || !io->done) return hipErrorInvalidValue;
+    dd::StepArgs p;
+    p.k = dd::make_consts(*cfg);
+    p.actions = io->actions;
+    p.reward = io->reward;
+    p.done = io->done;
+    p.obs = io->obs;
+    p.done_idx = io->done_idx;
+    p.done_count = io->done_count;
+    p.n = n;
+    if (st->precision == DD_F32) dd::launch_step_t<float>(p, io->action_format, *st, s);
+    else dd::launch_step_t<double>(p, io->action_format, *st, s);
+    return dd::finish();
+}
+
+int dd_reset(const DDConfig* cfg, const DDState* st, const uint8_t* mask, float* obs, int64_t n, void* stream) {
+    if (!cfg || !st || n < 0 || n > INT32_MAX) return hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (!dd::state_ok(st)) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 g((unsigned)dd::tiles_of(n)), b(dd::kBlock);
+    if (st->precision == DD_F32)
+        hipLaunchKernelGGL(dd::reset_kernel<float>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<float>(*st), mask, obs, n);
+    else
+        hipLaunchKernelGGL(dd::reset_kernel<double>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<double>(*st), mask, obs, n);
+    return dd::finish();
+}
+
+int dd_write_obs(const DDConfig* cfg, const DDState* st, float* obs, int64_t n, void* stream) {
+    if (!cfg || !st || n < 0 || n > INT32_MAX) return hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (!obs || !dd::state_ok(st)) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 g(dd::grid_of(n)), b(dd::kBlock);
+    if (st->precision == DD_F32)
+        hipLaunchKernelGGL(dd::obs_kernel<float>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<float>(*st), obs, n);
+    else
+        hipLaunchKernelGGL(dd::obs_kernel<double>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<double>(*st), obs, n);
+    return dd::finish();
+}
+
+int dd_get_info(const DDConfig* cfg, const DDState* st, void* distance, void* speed, int64_t n, void* stream) {
+    if (!cfg || !st || n < 0 || n > INT32_MAX) return hipErrorInvalidValue;
+    if (n == 0 || (!distance && !speed)) return 0;
+    if (!dd::state_ok(st)) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 g((unsigned)dd::tiles_of(n)), b(dd::kBlock);
+    if (st->precision == DD_F32)
+        hipLaunchKernelGGL(dd::info_kernel<float>, g, b, 0, s, dd::soa_of<float>(*st), (float*)distance,
+                           (float*)speed, n);
+    else
+        hipLaunchKernelGGL(dd::info_kernel<double>, g, b, 0, s, dd::soa_of<double>(*st), (double*)distance,
+                           (double*)speed, n);
+    return dd::finish();
+}
+
+int64_t dd_compact_workspace(int64_t n) { return n <= 0 ? 1 : dd::tiles_of(n); }
+
+int dd_compact(const uint8_t* flags, int32_t want, int32_t* idx_out, int32_t* count, int32_t* workspace,
+               int64_t n, void* stream) {
+    if (n < 0 || n > INT32_MAX || !count || (n > 0 && (!flags || !idx_out || !workspace)))
+        return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (n == 0) return (int)hipMemsetAsync(count, 0, sizeof(int32_t), s);
+    const int64_t m = dd::tiles_of(n);
+    hipLaunchKernelGGL(dd::compact_count_kernel, dim3((unsigned)m), dim3(dd::kBlock), 0, s, flags, want,
+                       workspace, n);
+    hipLaunchKernelGGL(dd::compact_scan_kernel, dim3(1), dim3(1024), 0, s, workspace, m, count);
+    hipLaunchKernelGGL(dd::compact_scatter_kernel, dim3((unsigned)m), dim3(dd::kBlock), 0, s, flags, want,
+                       (const int32_t*)workspace, idx_out, n);
+    return dd::finish();
+}
+
+int64_t dd_step_bytes_per_env(int32_t precision, int32_t action_format, int32_t with_obs) {
+    const int64_t f = precision == DD_F64 ? 8 : 4;
+    const int64_t act = action_format == DD_ACT_F32X3 ? 12 : action_format == DD_ACT_U8X3 ? 3 : 1;
+    // reads: x y vx vy angle omega fuel px py total (10 f) + status 1 + steps 4 + action
+    const int64_t rd = 10 * f + 1 + 4 + act;
+    // writes: x y vx vy angle omega fuel total reward (9 f) + steps 4 + done 1
+    // (status is rewritten only on the frame an episode ends)
+    const int64_t wr = 9 * f + 4 + 1;
+    return rd + wr + (with_obs ? DD_OBS_DIM * 4 : 0);
+}
+
+const char* dd_error_string(int code) { return hipGetErrorString((hipError_t)code); }
+
+int dd_abi_version(void) { return DD_ABI_VERSION; }
+
+}  // extern "C"

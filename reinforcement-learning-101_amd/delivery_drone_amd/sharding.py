@@ -1,0 +1,62 @@
+"""Sharding of one global drone batch over the GPUs of a node.
+
+Drones never interact (game_engine.py:95-138 touches only its own drone and
+platform), so the batch splits into contiguous blocks of global env ids, one
+block per rank, with no collective on the step path.  Spawn draws are keyed
+by the global id, so a drone's episodes do not depend on the world size.
+The only optional exchange is gathering observations to one rank
+(:func:`gather_obs`), over RCCL (backend ``"nccl"``) on the GPUs or gloo on
+the CPU.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["shard_bounds", "dist_env", "gather_obs"]
+
+
+def shard_bounds(total: int, rank: int, world: int) -> Tuple[int, int]:
+    """(first global id, count) of ``rank``'s block; the first ``total % world``
+    ranks hold one extra drone."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    if total < 0:
+        raise ValueError("total must be >= 0")
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def dist_env() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment (1 process: 0, 1, 0)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def gather_obs(obs: torch.Tensor, total: int, dst: int = 0, group=None) -> Optional[torch.Tensor]:
+    """Gather every rank's observation block ``[count_r, 15]`` into one
+    ``[total, 15]`` tensor on rank ``dst`` (None elsewhere).
+
+    Blocks are padded to the largest shard so a single ``gather`` call moves
+    them (one xGMI transfer per peer with RCCL)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    counts = [shard_bounds(total, r, world)[1] for r in range(world)]
+    if obs.shape[0] != counts[rank]:
+        raise ValueError(f"rank {rank} holds {obs.shape[0]} rows, its shard is {counts[rank]}")
+    width = max(counts) if counts else 0
+    padded = obs.new_zeros((width,) + tuple(obs.shape[1:]))
+    padded[: obs.shape[0]] = obs
+    gathered: Optional[List[torch.Tensor]] = None
+    if rank == dst:
+        gathered = [torch.empty_like(padded) for _ in range(world)]
+    dist.gather(padded, gather_list=gathered, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([g[:c] for g, c in zip(gathered, counts)], dim=0)

@@ -1,0 +1,84 @@
+"""Loading of the committed reference fixtures (tests/golden/) into SoA form.
+
+The fixtures were produced by tests/golden/make_golden.py from the reference
+engine itself; this module only reads them (numpy, allow_pickle=False; JSON).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+ST_DONE, ST_LANDED, ST_CRASHED, ST_PLAT_LEFT = 1, 2, 4, 8
+FLOAT_FIELDS = ("x", "y", "vx", "vy", "angle", "omega", "fuel", "px", "py", "total_reward")
+DYN_FIELDS = ("x", "y", "vx", "vy", "angle", "omega", "fuel", "px", "py")
+
+
+def npz(name: str) -> dict:
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
+
+
+def js(name: str):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def state_from_inputs(rec: dict) -> dict:
+    """SoA initial state (float64 / uint8 / int32 numpy) of a single-step fixture."""
+    st = {f: rec[f"in_{f}"].astype(np.float64) for f in DYN_FIELDS}
+    st["total_reward"] = rec["in_total"].astype(np.float64)
+    st["status"] = (rec["in_done"].astype(np.uint8) * ST_DONE
+                    + (rec["in_direction"] < 0).astype(np.uint8) * ST_PLAT_LEFT).astype(np.uint8)
+    st["steps"] = rec["in_steps"].astype(np.int32)
+    st["episode"] = np.zeros_like(st["steps"])
+    return st
+
+
+def expected_outputs(rec: dict) -> dict:
+    e = {f: rec[f"out_{f}"].astype(np.float64) for f in DYN_FIELDS}
+    e["total_reward"] = rec["out_total"].astype(np.float64)
+    e["reward"] = rec["out_reward"].astype(np.float64)
+    e["done"] = rec["out_done"].astype(bool)
+    e["landed"] = rec["out_landed"].astype(bool)
+    e["crashed"] = rec["out_crashed"].astype(bool)
+    e["plat_left"] = rec["out_direction"] < 0
+    e["steps"] = rec["out_steps"].astype(np.int64)
+    e["obs"] = rec["out_obs"].astype(np.float64)
+    e["info_distance"] = rec["out_info_distance"].astype(np.float64)
+    e["info_speed"] = rec["out_info_speed"].astype(np.float64)
+    return e
+
+
+def base_state(**kw) -> dict:
+    s = dict(x=400.0, y=100.0, vx=0.0, vy=0.0, angle=0.0, omega=0.0, fuel=1000.0, px=400.0, py=500.0,
+             steps=0, total=0.0, done=False, direction=1)
+    s.update(kw)
+    return s
+
+
+def edge_case_state(case: dict) -> dict:
+    """SoA (one lane) state of an edge_cases.json entry."""
+    s = case["state"]
+    st = {f: np.array([float(s[f])]) for f in DYN_FIELDS}
+    st["total_reward"] = np.array([float(s["total"])])
+    st["status"] = np.array([(ST_DONE if s["done"] else 0) | (ST_PLAT_LEFT if s["direction"] < 0 else 0)],
+                            dtype=np.uint8)
+    st["steps"] = np.array([int(s["steps"])], dtype=np.int32)
+    st["episode"] = np.zeros(1, dtype=np.int32)
+    return st
+
+
+def ulp32(a) -> np.ndarray:
+    """Spacing of float32 at |a| (as float64)."""
+    return np.spacing(np.abs(np.asarray(a, dtype=np.float32))).astype(np.float64)
+
+
+def f32_close(got, ref, ulps: float = 2.0, atol: float = 0.0) -> np.ndarray:
+    """|got - ref| <= ulps * ulp32(ref) + atol, elementwise (ref in double)."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    return np.abs(got - ref) <= ulps * ulp32(ref) + atol

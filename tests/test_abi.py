@@ -1,0 +1,128 @@
+"""CPU: the product library loads, exports the header's ABI, and validates
+arguments — without touching a GPU (no compute calls here)."""
+import ctypes
+import dataclasses
+import os
+import re
+import subprocess
+
+import pytest
+
+from delivery_drone_amd import abi
+from delivery_drone_amd.config import EnvConfig
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "dronestep.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dd_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_what_abi_binds():
+    assert header_functions() == sorted(abi.EXPORTS)
+
+
+def test_library_exports_every_header_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", abi.library_path()], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (dd_[a-z0-9_]+)$", out, flags=re.M))
+    missing = set(header_functions()) - exported
+    assert not missing, missing
+
+
+def test_library_is_gfx950_code():
+    blob = open(abi.library_path(), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the offload bundle's target id
+
+
+def test_library_loads_and_reports_abi():
+    lib = abi.lib()
+    assert lib.dd_abi_version() == abi.DD_ABI_VERSION
+
+
+def test_c_defaults_equal_envconfig_defaults():
+    """dd_config_default (C) vs EnvConfig (Python): also checks the ctypes
+    struct layout against the C one field by field."""
+    c = abi.DDConfig()
+    abi.lib().dd_config_default(ctypes.byref(c))
+    py = EnvConfig().to_abi()
+    for name, _ in abi.DDConfig._fields_:
+        assert getattr(c, name) == getattr(py, name), name
+    assert ctypes.sizeof(abi.DDConfig) == 32 * 8 + 18 * 4 + 8
+
+
+def test_envconfig_matches_reference_constants():
+    c = EnvConfig()
+    assert (c.gravity, c.drag, c.angular_drag) == (0.3, 0.99, 0.95)
+    assert (c.main_thrust_power, c.side_thrust_power, c.max_fuel) == (0.6, 0.3, 1000.0)
+    assert (c.platform_x_lo, c.platform_x_hi, c.platform_y_lo, c.platform_y_hi) == (100, 700, 100, 550)
+    assert (c.drone_x_min, c.drone_x_max, c.drone_y_min, c.drone_y_max) == (100, 700, 50, 250)
+    assert (c.ground_level, c.oob_margin, c.max_landing_velocity, c.max_landing_angle) == (550, 50, 3.0, 20.0)
+    assert c.randomize_platform and not c.randomize_drone and not c.auto_reset
+
+
+def test_envconfig_validation():
+    with pytest.raises(ValueError):
+        EnvConfig(platform_x_hi=100).validate()
+    with pytest.raises(ValueError):
+        EnvConfig(world_width=0).validate()
+    cfg = EnvConfig(seed=2**64 + 5).to_abi()
+    assert cfg.seed == 5
+    assert dataclasses.replace(EnvConfig(), auto_reset=True).to_abi().auto_reset == 1
+
+
+def _state(n_ptr=1, precision=abi.DD_F32):
+    p = ctypes.c_void_p(n_ptr)
+    return abi.DDState(p, p, p, p, p, p, p, p, p, p, p, p, p, 0, precision, 0)
+
+
+def test_argument_errors_return_invalid_value_without_gpu():
+    lib = abi.lib()
+    cfg = EnvConfig().to_abi()
+    io = abi.DDStepIO()
+    io.actions = io.reward = io.done = 1
+    EINVAL = 1  # hipErrorInvalidValue
+    assert lib.dd_step(None, ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state(precision=7)), ctypes.byref(io), 4, None) == EINVAL
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), -1, None) == EINVAL
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 2**31, None) == EINVAL
+    bad = abi.DDState()  # null pointers
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(bad), ctypes.byref(io), 4, None) == EINVAL
+    io.action_format = 9
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
+    io.action_format = 0
+    io.done_idx = 8  # done_idx without done_count
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
+    assert lib.dd_reset(ctypes.byref(cfg), ctypes.byref(bad), None, None, 4, None) == EINVAL
+    assert lib.dd_write_obs(ctypes.byref(cfg), ctypes.byref(_state()), None, 4, None) == EINVAL
+    assert lib.dd_reset(ctypes.byref(cfg), ctypes.byref(bad), None, None, 0, None) == 0  # empty batch
+    assert lib.dd_compact(None, 0, None, None, None, 4, None) == EINVAL
+    assert lib.dd_error_string(EINVAL)
+
+
+def test_byte_model():
+    lib = abi.lib()
+    # f32, bitmask actions, obs: reads 10*4+1+4+1, writes 9*4+4+1, obs 60
+    assert lib.dd_step_bytes_per_env(abi.DD_F32, abi.DD_ACT_BITMASK, 1) == 46 + 41 + 60
+    assert lib.dd_step_bytes_per_env(abi.DD_F32, abi.DD_ACT_BITMASK, 0) == 87
+    assert lib.dd_step_bytes_per_env(abi.DD_F64, abi.DD_ACT_F32X3, 1) == (80 + 5 + 12) + (72 + 5) + 60
+    assert lib.dd_compact_workspace(1000) == 4
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    from delivery_drone_amd import VecDroneEnv
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        VecDroneEnv(8)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(abi, "_LIB", None)
+    monkeypatch.setattr(abi, "library_path", lambda: str(tmp_path / "nope.so"))
+    with pytest.raises(abi.NativeLibraryError, match="not built"):
+        abi.lib()

@@ -1,0 +1,416 @@
+"""GPU: the HIP path (through the C ABI) against the reference fixtures and the
+oracle, on identical inputs.
+
+Tolerances:
+* f64 storage: state / reward / obs within 4 double ulps of the reference
+  (|d| <= 4 ulp(ref) + 1e-12 absolute for cancellations near 0); flags exact.
+  The kernel does the reference's double arithmetic; differences come only
+  from device sin/cos vs glibc (<= 1 ulp) and v*v vs glibc pow(v, 2) (1 ulp
+  on ~0.09 % of squares).
+* f32 storage: the same double result rounded once to float32, so within
+  1 float32 ulp of the reference (2 allowed) and flags exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_data as gd
+from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
+from oracle import oracle as ora
+
+pytestmark = pytest.mark.gpu
+
+
+def load(env: VecDroneEnv, st: dict):
+    for k, v in st.items():
+        t = getattr(env, k)
+        t.copy_(torch.as_tensor(np.asarray(v), dtype=t.dtype))
+
+
+def f64_close(got, ref, ulps=4, atol=1e-12):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return np.abs(got - ref) <= ulps * np.spacing(np.abs(ref)) + atol
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def step_fixture(rec, precision, device, action_format="bitmask", **cfg):
+    n = rec["in_x"].shape[0]
+    env = VecDroneEnv(n, precision=precision, device=device, config=EnvConfig(**cfg))
+    load(env, gd.state_from_inputs(rec))
+    a = torch.as_tensor(rec["in_action"], device=device)
+    if action_format == "f32x3":
+        a = torch.stack([(a >> k) & 1 for k in range(3)], dim=1).float()
+    elif action_format == "u8x3":
+        a = torch.stack([(a >> k) & 1 for k in range(3)], dim=1).to(torch.uint8)
+    elif action_format == "boolx3":
+        a = torch.stack([(a >> k) & 1 for k in range(3)], dim=1).bool()
+    obs, reward, done, info = env.step(a)
+    torch.cuda.synchronize()
+    return env, host(obs), host(reward), host(done), info
+
+
+def check_vs_reference(env, obs, reward, done, info, e, precision):
+    close = (lambda g, r: f64_close(g, r)) if precision == "f64" else (lambda g, r: gd.f32_close(g, r, 2.0))
+    np.testing.assert_array_equal(done, e["done"])
+    status = host(env.status)
+    np.testing.assert_array_equal((status & gd.ST_LANDED) != 0, e["landed"])
+    np.testing.assert_array_equal((status & gd.ST_CRASHED) != 0, e["crashed"])
+    np.testing.assert_array_equal(host(env.steps), e["steps"])
+    for f in gd.DYN_FIELDS + ("total_reward",):
+        ok = close(host(getattr(env, f)), e[f])
+        assert ok.all(), (f, np.flatnonzero(~ok)[:5])
+    assert close(reward, e["reward"]).all()
+    ok = gd.f32_close(obs, e["obs"], 2.0)  # obs is float32 in both precisions
+    assert ok.all(), np.argwhere(~ok)[:5]
+    ok_d = close(host(info["distance_to_platform"]), e["info_distance"])
+    ok_s = close(host(info["speed"]), e["info_speed"])
+    assert ok_d.all() and ok_s.all()
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_single_step_vs_reference(precision, gpu_device):
+    rec = gd.npz("single_step.npz")
+    env, obs, reward, done, info = step_fixture(rec, precision, gpu_device)
+    check_vs_reference(env, obs, reward, done, info, gd.expected_outputs(rec), precision)
+
+
+@pytest.mark.parametrize("fmt", ["f32x3", "u8x3", "boolx3"])
+def test_action_formats_match_bitmask(fmt, gpu_device):
+    rec = gd.npz("single_step.npz")
+    ref = step_fixture(rec, "f32", gpu_device)
+    alt = step_fixture(rec, "f32", gpu_device, action_format=fmt)
+    for a, b in zip(ref[1:4], alt[1:4]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_moving_platform_vs_reference(gpu_device):
+    rec = gd.npz("single_step_moving.npz")
+    e = gd.expected_outputs(rec)
+    env, obs, reward, done, info = step_fixture(rec, "f64", gpu_device, platform_moving=True)
+    check_vs_reference(env, obs, reward, done, info, e, "f64")
+    np.testing.assert_array_equal((host(env.status) & gd.ST_PLAT_LEFT) != 0, e["plat_left"])
+
+
+def test_wind_vs_reference(gpu_device):
+    rec = gd.npz("single_step_wind.npz")
+    env, obs, reward, done, info = step_fixture(rec, "f64", gpu_device, wind_enabled=True,
+                                                wind_x=float(rec["in_wind_x"]), wind_y=float(rec["in_wind_y"]))
+    check_vs_reference(env, obs, reward, done, info, gd.expected_outputs(rec), "f64")
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_edge_cases_vs_reference(precision, gpu_device):
+    for case in gd.js("edge_cases.json"):
+        if case["f64_only"] and precision == "f32":
+            continue
+        env = VecDroneEnv(1, precision=precision, device=gpu_device)
+        load(env, gd.edge_case_state(case))
+        obs, reward, done, info = env.step(torch.tensor([case["action"]], dtype=torch.uint8, device=gpu_device))
+        x = case["expect"]
+        st = int(env.status[0].item())
+        assert bool(done[0].item()) == x["done"], case["name"]
+        assert bool(st & gd.ST_LANDED) == x["landed"] and bool(st & gd.ST_CRASHED) == x["crashed"], case["name"]
+        assert int(env.steps[0].item()) == x["steps"], case["name"]
+        close = f64_close if precision == "f64" else (lambda g, r: gd.f32_close(g, r, 2.0))
+        for f in ("x", "y", "vx", "vy", "angle", "omega", "fuel"):
+            assert close(getattr(env, f)[0].item(), x[f]), (case["name"], f)
+        assert close(reward[0].item(), x["reward"]), case["name"]
+        assert gd.f32_close(host(obs[0]), x["obs"], 2.0).all(), case["name"]
+
+
+def test_notebook_kats(gpu_device):
+    for name, k in gd.js("kat_notebooks.json").items():
+        env = VecDroneEnv(1, precision="f64", device=gpu_device)
+        load(env, gd.edge_case_state({"state": gd.base_state(**k["start"])}))
+        a = torch.tensor([k["action"]], dtype=torch.uint8, device=gpu_device)
+        for _ in range(k["frames"]):
+            obs, reward, done, info = env.step(a)
+        row = dict(zip(("drone_x", "drone_y", "drone_vx", "drone_vy", "drone_angle", "drone_angular_vel",
+                        "drone_fuel", "platform_x", "platform_y", "distance_to_platform", "dx_to_platform",
+                        "dy_to_platform", "speed"), host(obs[0])))
+        got = dict(row, reward=reward[0].item(), total_reward=env.total_reward[0].item(),
+                   info_angle=env.angle[0].item(), info_distance=info["distance_to_platform"][0].item(),
+                   info_speed=info["speed"][0].item(), steps=int(env.steps[0].item()))
+        for key, want in k["expect"].items():
+            if key in row:  # obs leaves as float32
+                assert gd.f32_close(got[key], want, 1.0), (name, key, got[key], want)
+            elif key == "steps":
+                assert got[key] == want
+            else:
+                assert f64_close(got[key], want), (name, key, got[key], want)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_vs_oracle_same_precision(precision, gpu_device):
+    """Broad random states: GPU vs the C oracle with the same storage width."""
+    rng = np.random.default_rng(3)
+    n = 100_003  # ragged: not a multiple of the 256-lane tile
+    rec = gd.npz("single_step.npz")
+    idx = rng.integers(0, rec["in_x"].shape[0], n)
+    st = {k: v[idx] for k, v in gd.state_from_inputs(rec).items()}
+    st["x"] = st["x"] + rng.uniform(-5, 5, n)  # new values (double) around the fixture states
+    st["vy"] = st["vy"] + rng.uniform(-0.5, 0.5, n)
+    dt = np.float64 if precision == "f64" else np.float32
+    st = {k: (v.astype(dt) if v.dtype == np.float64 else v) for k, v in st.items()}
+    acts = rng.integers(0, 8, n).astype(np.uint8)
+    cfg = EnvConfig(auto_reset=True, randomize_drone=True, seed=9)
+    env = VecDroneEnv(n, precision=precision, device=gpu_device, config=cfg)
+    oenv = ora.OracleEnv(n, precision=precision, config=cfg)
+    load(env, st)
+    oenv.load_state_dict(st)
+    for t in range(3):
+        obs, reward, done, _ = env.step(torch.as_tensor(acts, device=gpu_device))
+        oobs, oreward, odone, _ = oenv.step(acts)
+        np.testing.assert_array_equal(host(done), odone)
+        np.testing.assert_array_equal(host(env.status), oenv.status)
+        np.testing.assert_array_equal(host(env.steps), oenv.steps)
+        np.testing.assert_array_equal(host(env.episode), oenv.episode)
+        ulps = 1.0
+        if precision == "f64":
+            for f in gd.FLOAT_FIELDS:
+                assert f64_close(host(getattr(env, f)), getattr(oenv, f)).all(), f
+        else:
+            for f in gd.FLOAT_FIELDS:
+                assert gd.f32_close(host(getattr(env, f)), getattr(oenv, f), ulps).all(), f
+        assert gd.f32_close(host(obs), oobs, 1.0).all()
+        acts = rng.integers(0, 8, n).astype(np.uint8)
+
+
+def replay(t, precision, device, **cfg):
+    T, B = t["actions"].shape
+    env = VecDroneEnv(B, precision=precision, device=device, config=EnvConfig(**cfg))
+
+    def set_lane(b, x, y, px, py):
+        for f, v in (("x", x), ("y", y), ("px", px), ("py", py)):
+            getattr(env, f)[b] = v
+        for f in ("vx", "vy", "angle", "omega", "total_reward"):
+            getattr(env, f)[b] = 0
+        env.fuel[b] = env.config.max_fuel
+        env.status[b] = 0
+        env.steps[b] = 0
+
+    for b in range(B):
+        set_lane(b, *t["spawn0"][b])
+    ev = {}
+    for row in t["events"]:
+        ev.setdefault(int(row[0]), []).append(row[1:])
+    worst, flag_mismatch = 0.0, 0
+    acts = torch.as_tensor(t["actions"], device=device)
+    for i in range(T):
+        obs, reward, done, _ = env.step(acts[i])
+        worst = max(worst, float(np.max(np.abs(host(obs).astype(np.float64) - t["obs"][i]))))
+        flag_mismatch += int((host(done) != t["done"][i]).sum())
+        for b, x, y, px, py in ev.get(i, []):
+            set_lane(int(b), x, y, px, py)
+    return worst, flag_mismatch
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("name,cfg", [("traj_random.npz", {}), ("traj_moving.npz", {"platform_moving": True})])
+def test_trajectories_vs_reference(name, cfg, precision, gpu_device):
+    t = gd.npz(name)
+    worst, flag_mismatch = replay(t, precision, gpu_device, **cfg)
+    assert flag_mismatch == 0
+    # obs leave as float32: 1e-6 covers float32 rounding of values < 8;
+    # f32 storage adds the drift of float32 state over ~400 frames
+    assert worst < (2e-6 if precision == "f64" else 1e-4), worst
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_config1_trajectory(precision, gpu_device):
+    """Config 1 (1000 frames, fixed spawn, reset on done) replayed on the GPU."""
+    t = gd.npz("traj_fixed.npz")
+    env = VecDroneEnv(1, precision=precision, device=gpu_device, randomize_drone=False,
+                      randomize_platform=False)
+    env.reset()
+    acts = torch.as_tensor(t["actions"], device=gpu_device)
+    worst = 0.0
+    for i in range(acts.shape[0]):
+        obs, reward, done, _ = env.step(acts[i:i + 1])
+        worst = max(worst, float(np.max(np.abs(host(obs[0]).astype(np.float64) - t["obs"][i]))))
+        assert bool(done[0].item()) == bool(t["done"][i]), i
+        if done[0].item():
+            env.reset()
+            assert gd.f32_close(host(env.obs[0]), t["reset_obs"][i], 1.0).all()
+    assert worst < (2e-6 if precision == "f64" else 1e-4), worst
+
+
+def test_sticky_done_and_needs_reset(gpu_device):
+    env = VecDroneEnv(4, device=gpu_device, randomize_platform=False)
+    env.reset()
+    env.y.fill_(700.0)  # below the world: crash next frame
+    a = torch.zeros(4, dtype=torch.uint8, device=gpu_device)
+    _, r1, d1, _ = env.step(a)
+    assert d1.all() and (r1 < -99).all()
+    before = {f: getattr(env, f).clone() for f in ("x", "y", "vx", "vy", "steps", "total_reward")}
+    _, r2, d2, info = env.step(a)
+    assert d2.all() and (r2 == 0).all() and info["needs_reset"].all()
+    for f, v in before.items():
+        assert torch.equal(getattr(env, f), v), f
+
+
+def test_auto_reset_next_step(gpu_device):
+    cfg = dict(auto_reset=True, randomize_drone=True, seed=4)
+    env = VecDroneEnv(3, device=gpu_device, **cfg)
+    env.reset()
+    ep0 = env.episode.clone()
+    env.y.fill_(700.0)
+    a = torch.zeros(3, dtype=torch.uint8, device=gpu_device)
+    _, r1, d1, _ = env.step(a)
+    assert d1.all()
+    obs, r2, d2, _ = env.step(a)
+    assert (~d2).all() and (r2 == 0).all()
+    assert torch.equal(env.episode, ep0 + 1) and (env.steps == 0).all()
+    o = ora.OracleEnv(3, precision="f32", config=EnvConfig(**cfg))
+    o.episode[:] = host(ep0)  # the oracle draws the same Philox spawn for (env, episode)
+    oobs, _ = o.reset()
+    np.testing.assert_array_equal(host(obs), oobs)
+
+
+def test_reset_matches_oracle_and_ranges(gpu_device):
+    facts = gd.js("reset_facts.json")
+    n = 200_000
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, seed=11)
+    env = VecDroneEnv(n, device=gpu_device, config=cfg, precision="f64")
+    obs = env.reset()
+    o = ora.OracleEnv(n, precision="f64", config=cfg)
+    oobs, _ = o.reset()
+    for f in gd.FLOAT_FIELDS:
+        np.testing.assert_array_equal(host(getattr(env, f)), getattr(o, f), err_msg=f)
+    np.testing.assert_array_equal(host(obs), oobs)
+    for f, key in (("x", "drone_x"), ("y", "drone_y"), ("px", "platform_x"), ("py", "platform_y")):
+        v = host(getattr(env, f))
+        assert [int(v.min()), int(v.max())] == facts[key]
+    # determinism and masked reset
+    m = torch.zeros(n, dtype=torch.bool, device=gpu_device)
+    m[::7] = True
+    x_before = env.x.clone()
+    env.reset(m)
+    assert torch.equal(env.x[~m], x_before[~m])
+    assert (env.episode[m] == 2).all() and (env.episode[~m] == 1).all()
+
+
+def test_sharding_invariance(gpu_device):
+    cfg = EnvConfig(randomize_drone=True, auto_reset=True, seed=21)
+    full = VecDroneEnv(1000, device=gpu_device, config=cfg)
+    parts = [VecDroneEnv(300, device=gpu_device, config=cfg),
+             VecDroneEnv(700, device=gpu_device, config=cfg, env_id_base=300)]
+    for e in [full] + parts:
+        e.reset()
+    g = torch.Generator(device=gpu_device).manual_seed(0)
+    for _ in range(400):
+        a = torch.randint(0, 8, (1000,), device=gpu_device, generator=g, dtype=torch.uint8)
+        of, rf, df, _ = full.step(a)
+        oa, ra, da, _ = parts[0].step(a[:300])
+        ob, rb, db, _ = parts[1].step(a[300:])
+        assert torch.equal(of, torch.cat([oa, ob])) and torch.equal(df, torch.cat([da, db]))
+    assert int(full.episode.max()) > 1
+
+
+def test_done_idx_compaction(gpu_device):
+    n = 50_000
+    env = VecDroneEnv(n, device=gpu_device, randomize_drone=True, seed=2)
+    env.reset()
+    g = torch.Generator(device=gpu_device).manual_seed(1)
+    seen = 0
+    for _ in range(200):
+        was_done = env.done.clone()
+        a = torch.randint(0, 8, (n,), device=gpu_device, generator=g, dtype=torch.uint8)
+        _, _, done, info = env.step(a, collect_done_idx=True)
+        newly = torch.nonzero(done & ~was_done).flatten().to(torch.int32)
+        got = torch.sort(info["done_idx"]).values
+        assert torch.equal(got, newly)
+        seen += newly.numel()
+    assert seen > 1000
+
+
+def test_active_indices_ordered(gpu_device):
+    for n in (1, 255, 256, 257, 70_001):
+        env = VecDroneEnv(n, device=gpu_device)
+        flags = torch.rand(n, device=gpu_device) < 0.3
+        idx = env.active_indices(flags)
+        assert torch.equal(idx.long(), torch.nonzero(~flags).flatten())
+
+
+def test_empty_and_tiny_batches(gpu_device):
+    env = VecDroneEnv(0, device=gpu_device)
+    obs, reward, done, _ = env.step(torch.zeros(0, dtype=torch.uint8, device=gpu_device))
+    assert obs.shape == (0, 15) and env.reset().shape == (0, 15)
+    assert env.active_indices().numel() == 0
+    env1 = VecDroneEnv(1, device=gpu_device)
+    env1.reset()
+    env1.step(torch.ones(1, dtype=torch.uint8, device=gpu_device))
+    assert int(env1.steps[0]) == 1
+
+
+def test_obs_matches_get_state_and_lane_slices(gpu_device):
+    n = 4099
+    env = VecDroneEnv(n, device=gpu_device, randomize_drone=True, seed=8)
+    env.reset()
+    a = torch.randint(0, 8, (n,), device=gpu_device, dtype=torch.uint8)
+    obs, _, _, _ = env.step(a)
+    step_obs = obs.clone()
+    assert torch.equal(env.get_state(), step_obs)
+    # stepping a lane range equals stepping those lanes in a full batch
+    env2 = VecDroneEnv(n, device=gpu_device, randomize_drone=True, seed=8)
+    env2.reset()
+    env2.step(a[:1000], lanes=slice(0, 1000))
+    env2.step(a[1000:], lanes=slice(1000, n))
+    assert torch.equal(env2.get_state(), step_obs)
+
+
+def test_hipgraph_capture_matches_eager(gpu_device):
+    n, k = 65_536, 16
+    cfg = dict(randomize_drone=True, auto_reset=True, seed=6)
+    eager = VecDroneEnv(n, device=gpu_device, **cfg)
+    graphed = VecDroneEnv(n, device=gpu_device, **cfg)
+    eager.reset()
+    graphed.reset()
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
+    s = torch.cuda.Stream(gpu_device)
+    s.wait_stream(torch.cuda.current_stream(gpu_device))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        for i in range(k):
+            graphed.step(acts[i])
+    graphed.load_state_dict(eager.state_dict())
+    graph.replay()
+    for i in range(k):
+        eager.step(acts[i])
+    torch.cuda.synchronize()
+    assert torch.equal(graphed.obs, eager.obs)
+    for f in gd.FLOAT_FIELDS + ("status", "steps", "episode"):
+        assert torch.equal(getattr(graphed, f), getattr(eager, f)), f
+
+
+def test_large_batch_properties(gpu_device):
+    """BASELINE-scale batch: a sampled slice against the oracle, plus
+    size-independent invariants over all lanes."""
+    n = 1 << 22
+    cfg = EnvConfig(randomize_drone=True, auto_reset=True, seed=13)
+    env = VecDroneEnv(n, device=gpu_device, config=cfg)
+    env.reset()
+    g = torch.Generator(device=gpu_device).manual_seed(5)
+    for _ in range(20):
+        a = torch.randint(0, 8, (n,), device=gpu_device, generator=g, dtype=torch.uint8)
+        obs, reward, done, _ = env.step(a)
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs).all() and torch.isfinite(reward).all()
+    assert (env.fuel >= 0).all() and (env.fuel <= 1000).all()
+    assert (env.angle.abs() <= 180).all()
+    assert ((reward > -101) & (reward < 100)).all()
+    # one more frame on a contiguous window, compared with the oracle
+    lo, m = n - 70_000, 70_000
+    st = {f: host(getattr(env, f))[lo:] for f in gd.FLOAT_FIELDS + ("status", "steps", "episode")}
+    o = ora.OracleEnv(m, precision="f32", config=cfg, env_id_base=lo)
+    o.load_state_dict(st)
+    a = torch.randint(0, 8, (n,), device=gpu_device, generator=g, dtype=torch.uint8)
+    obs, reward, done, _ = env.step(a)
+    oobs, oreward, odone, _ = o.step(host(a)[lo:])
+    np.testing.assert_array_equal(host(done)[lo:], odone)
+    assert gd.f32_close(host(obs)[lo:], oobs, 1.0).all()
+    assert gd.f32_close(host(reward)[lo:], oreward, 1.0).all()

@@ -1,0 +1,252 @@
+"""CPU: the oracle (oracle/drone_oracle.c) reproduces the reference's fixtures.
+
+This pins the checker before any GPU result is trusted.  In double precision
+the oracle must equal the reference bit for bit (it performs the same libm
+calls in the same order).  In float32 storage mode — the GPU's default — it
+must stay within 2 float32 ulps with identical done/landed/crashed flags.
+"""
+import numpy as np
+import pytest
+
+import golden_data as gd
+from oracle import oracle as ora
+
+
+def run_single(rec, precision="f64", **cfg):
+    n = rec["in_x"].shape[0]
+    env = ora.OracleEnv(n, precision=precision, **cfg)
+    st = gd.state_from_inputs(rec)
+    env.load_state_dict(st)
+    obs, reward, done, obs64 = env.step(rec["in_action"])
+    return env, obs, reward, done, obs64
+
+
+def check_exact(env, reward, done, obs64, e, ignore=()):
+    for f in gd.DYN_FIELDS + ("total_reward",):
+        if f in ignore:
+            continue
+        np.testing.assert_array_equal(getattr(env, f), e[f], err_msg=f)
+    np.testing.assert_array_equal(reward, e["reward"])
+    np.testing.assert_array_equal(done, e["done"])
+    np.testing.assert_array_equal((env.status & gd.ST_LANDED) != 0, e["landed"])
+    np.testing.assert_array_equal((env.status & gd.ST_CRASHED) != 0, e["crashed"])
+    np.testing.assert_array_equal(env.steps, e["steps"])
+    np.testing.assert_array_equal(obs64, e["obs"])
+    d, s = env.get_info()
+    np.testing.assert_array_equal(d, e["info_distance"])
+    np.testing.assert_array_equal(s, e["info_speed"])
+
+
+@pytest.mark.parametrize("name,cfg", [
+    ("single_step.npz", {}),
+    ("single_step_moving.npz", {"platform_moving": True}),
+])
+def test_oracle_f64_bit_exact(name, cfg):
+    rec = gd.npz(name)
+    env, obs, reward, done, obs64 = run_single(rec, **cfg)
+    e = gd.expected_outputs(rec)
+    check_exact(env, reward, done, obs64, e)
+    if cfg.get("platform_moving"):
+        np.testing.assert_array_equal((env.status & gd.ST_PLAT_LEFT) != 0, e["plat_left"])
+
+
+def test_oracle_f64_wind():
+    rec = gd.npz("single_step_wind.npz")
+    env, obs, reward, done, obs64 = run_single(rec, wind_enabled=True, wind_x=float(rec["in_wind_x"]),
+                                               wind_y=float(rec["in_wind_y"]))
+    check_exact(env, reward, done, obs64, gd.expected_outputs(rec))
+
+
+def test_oracle_f32_storage_within_2ulp():
+    rec = gd.npz("single_step.npz")
+    env, obs, reward, done, obs64 = run_single(rec, precision="f32")
+    e = gd.expected_outputs(rec)
+    np.testing.assert_array_equal(done, e["done"])
+    np.testing.assert_array_equal((env.status & gd.ST_LANDED) != 0, e["landed"])
+    np.testing.assert_array_equal((env.status & gd.ST_CRASHED) != 0, e["crashed"])
+    for f in gd.DYN_FIELDS + ("total_reward",):
+        assert gd.f32_close(getattr(env, f), e[f], 1.0).all(), f
+    assert gd.f32_close(reward, e["reward"], 1.0).all()
+    assert gd.f32_close(obs, e["obs"], 1.0).all()
+
+
+def test_oracle_edge_cases():
+    for case in gd.js("edge_cases.json"):
+        env = ora.OracleEnv(1, precision="f64")
+        env.load_state_dict(gd.edge_case_state(case))
+        obs, reward, done, obs64 = env.step([case["action"]])
+        x = case["expect"]
+        for f in ("x", "y", "vx", "vy", "angle", "omega", "fuel"):
+            assert getattr(env, f)[0] == x[f], (case["name"], f)
+        assert reward[0] == x["reward"], case["name"]
+        assert bool(done[0]) == x["done"], case["name"]
+        assert bool(env.status[0] & gd.ST_LANDED) == x["landed"], case["name"]
+        assert bool(env.status[0] & gd.ST_CRASHED) == x["crashed"], case["name"]
+        assert env.steps[0] == x["steps"], case["name"]
+        assert list(obs64[0]) == x["obs"], case["name"]
+
+
+def test_edge_cases_cover_survey_a16():
+    names = {c["name"]: c["expect"] for c in gd.js("edge_cases.json")}
+    assert names["spawn_over_pad_lands"]["reward"] == pytest.approx(99.9) and names["spawn_over_pad_lands"]["landed"]
+    assert names["fuel1_main_left"]["fuel"] == 0 and names["fuel1_main_left"]["omega"] == 0.0
+    assert names["fuel1_main_left"]["reward"] == pytest.approx(-50.1)
+    assert names["angle_wrap_pos"]["angle"] == -178.0
+    assert names["ground_off_pad"]["reward"] == pytest.approx(-100.1)
+    assert names["oob_left"]["reward"] == pytest.approx(-50.1)
+    assert not names["on_pad_fast_above_ground"]["done"]
+    assert names["on_pad_fast_below_ground"]["crashed"]
+    assert names["landing_beats_fuel_out"]["landed"] and names["landing_beats_fuel_out"]["fuel"] == 0
+    sticky = names["sticky_done"]
+    assert sticky["reward"] == 0 and sticky["done"] and sticky["needs_reset"] and sticky["steps"] == 17
+    assert names["far_shaping_negative"]["reward"] < -0.1
+
+
+def test_oracle_notebook_kats():
+    kats = gd.js("kat_notebooks.json")
+    keys = ("drone_x", "drone_y", "drone_vx", "drone_vy", "drone_angle", "drone_angular_vel", "drone_fuel",
+            "platform_x", "platform_y", "distance_to_platform", "dx_to_platform", "dy_to_platform", "speed")
+    for name, k in kats.items():
+        env = ora.OracleEnv(1, precision="f64")
+        s = gd.base_state(**k["start"])
+        env.load_state_dict(gd.edge_case_state({"state": s}))
+        for _ in range(k["frames"]):
+            obs, reward, done, obs64 = env.step([k["action"]])
+        got = dict(zip(keys, obs64[0]))
+        got["reward"] = reward[0]
+        got["total_reward"] = env.total_reward[0]
+        got["info_angle"] = env.angle[0]
+        d, s = env.get_info()
+        got["info_distance"], got["info_speed"] = d[0], s[0]
+        got["steps"] = env.steps[0]
+        for key, want in k["expect"].items():
+            assert got[key] == want, (name, key, got[key], want)
+
+
+def test_oracle_config1_trajectory():
+    """Config 1: 1000 frames, fixed spawn, reset on done — bit-exact in f64."""
+    t = gd.npz("traj_fixed.npz")
+    env = ora.OracleEnv(1, precision="f64", randomize_drone=False, randomize_platform=False)
+    env.reset()
+    for i, a in enumerate(t["actions"]):
+        obs, reward, done, obs64 = env.step([a])
+        np.testing.assert_array_equal(obs64[0], t["obs"][i], err_msg=f"frame {i}")
+        assert reward[0] == t["reward"][i] and bool(done[0]) == bool(t["done"][i]), i
+        if done[0]:
+            _, r64 = env.reset()
+            np.testing.assert_array_equal(r64[0], t["reset_obs"][i])
+    assert t["done"].sum() >= 3  # several episodes inside the 1000 frames
+
+
+def replay_batch(t, env, set_lane):
+    """Replay traj_random-style fixtures: inject each recorded spawn."""
+    T, B = t["actions"].shape
+    for b in range(B):
+        set_lane(b, *t["spawn0"][b])
+    ev = {}
+    for row in t["events"]:
+        ev.setdefault(int(row[0]), []).append(row[1:])
+    worst = 0.0
+    flags_equal = 0
+    for i in range(T):
+        obs64, reward, done = env(t["actions"][i])
+        worst = max(worst, float(np.max(np.abs(obs64 - t["obs"][i]))))
+        flags_equal += int(np.array_equal(done, t["done"][i]))
+        for b, x, y, px, py in ev.get(i, []):
+            set_lane(int(b), x, y, px, py)
+    return worst, flags_equal
+
+
+def make_oracle_replayer(B, precision, **cfg):
+    env = ora.OracleEnv(B, precision=precision, **cfg)
+
+    def set_lane(b, x, y, px, py):
+        for f, v in (("x", x), ("y", y), ("px", px), ("py", py)):
+            getattr(env, f)[b] = v
+        for f in ("vx", "vy", "angle", "omega", "total_reward"):
+            getattr(env, f)[b] = 0
+        env.fuel[b] = env.cfg.max_fuel
+        env.status[b] = 0
+        env.steps[b] = 0
+
+    def stepper(a):
+        obs, reward, done, obs64 = env.step(a)
+        return obs64, reward, done
+
+    return stepper, set_lane
+
+
+@pytest.mark.parametrize("name,cfg", [("traj_random.npz", {}), ("traj_moving.npz", {"platform_moving": True})])
+def test_oracle_batch_trajectories(name, cfg):
+    t = gd.npz(name)
+    stepper, set_lane = make_oracle_replayer(t["actions"].shape[1], "f64", **cfg)
+    worst, flags_equal = replay_batch(t, stepper, set_lane)
+    assert worst == 0.0
+    assert flags_equal == t["actions"].shape[0]
+
+
+def test_oracle_f32_trajectory_tracks_reference():
+    t = gd.npz("traj_random.npz")
+    stepper, set_lane = make_oracle_replayer(t["actions"].shape[1], "f32")
+    worst, flags_equal = replay_batch(t, stepper, set_lane)
+    assert flags_equal == t["actions"].shape[0]
+    assert worst < 1e-4
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors for philox4x32-10
+    assert list(ora.philox4x32_10([0, 0, 0, 0], [0, 0])) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert list(ora.philox4x32_10([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2)) == [
+        0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert list(ora.philox4x32_10([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344],
+                                  [0xA4093822, 0x299F31D0])) == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_oracle_reset_ranges_match_reference():
+    facts = gd.js("reset_facts.json")
+    env = ora.OracleEnv(facts["draws"], precision="f64", randomize_drone=True, randomize_platform=True, seed=3)
+    env.reset()
+    for f, key in (("x", "drone_x"), ("y", "drone_y"), ("px", "platform_x"), ("py", "platform_y")):
+        v = getattr(env, f)
+        assert [int(v.min()), int(v.max())] == facts[key], f
+        assert np.all(v == np.round(v))
+    assert np.all(env.episode == 1)
+    fixed = ora.OracleEnv(3, precision="f64", randomize_drone=False, randomize_platform=False)
+    obs, obs64 = fixed.reset()
+    assert [fixed.x[0], fixed.y[0]] == facts["fixed_drone"]
+    assert [fixed.px[0], fixed.py[0]] == facts["fixed_platform"]
+    assert list(np.concatenate([obs64[0, 2:7], obs64[0, 12:]])) == facts["reset_obs_tail"]
+
+
+def test_oracle_reset_uniformity_chi2():
+    """Spawn draws are uniform over the reference's integer ranges."""
+    n = 200_000
+    env = ora.OracleEnv(n, precision="f64", randomize_drone=True, randomize_platform=True, seed=11)
+    env.reset()
+    for f, lo, hi in (("x", 100, 700), ("y", 50, 250), ("px", 100, 699), ("py", 100, 549)):
+        k = hi - lo + 1
+        counts = np.bincount((getattr(env, f) - lo).astype(np.int64), minlength=k)
+        assert counts.shape[0] == k and counts.min() > 0
+        exp = n / k
+        chi2 = float(((counts - exp) ** 2 / exp).sum())
+        # df = k - 1; mean df, sd sqrt(2 df): accept within 5 sd
+        assert abs(chi2 - (k - 1)) < 5 * np.sqrt(2 * (k - 1)), (f, chi2, k)
+
+
+def test_oracle_sharding_invariance():
+    """Global env ids key the spawns: two shards == one batch."""
+    cfg = dict(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=5, precision="f32")
+    full = ora.OracleEnv(1000, **cfg)
+    a = ora.OracleEnv(400, **cfg)
+    b = ora.OracleEnv(600, env_id_base=400, **cfg)
+    for e in (full, a, b):
+        e.reset()
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        act = rng.integers(0, 8, 1000).astype(np.uint8)
+        of, rf, df, _ = full.step(act)
+        oa, ra, da, _ = a.step(act[:400])
+        ob, rb, db, _ = b.step(act[400:])
+        np.testing.assert_array_equal(of, np.concatenate([oa, ob]))
+        np.testing.assert_array_equal(rf, np.concatenate([ra, rb]))
+    assert full.episode.max() > 1  # auto-reset happened
