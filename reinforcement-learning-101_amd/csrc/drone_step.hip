@@ -87,9 +87,18 @@ __device__ __forceinline__ double div_exact(double x, double d, double inv_d) {
 // The per-lane state, widened to double for the frame's arithmetic.
 struct Lane {
     double x, y, vx, vy, angle, omega, fuel, px, py, total;
+    double speed, dist;  // derived: Drone.get_speed, physics.distance to the pad
     uint32_t status;
     int32_t steps, episode;
 };
+
+// Drone.get_speed (drone.py:139-145) and physics.distance (physics.py:42-44)
+// of the current state; both the reward and get_state use them.
+__device__ __forceinline__ void measure(Lane& s) {
+    const double dx = s.px - s.x, dy = s.py - s.y;
+    s.speed = sqrt(s.vx * s.vx + s.vy * s.vy);
+    s.dist = sqrt(dx * dx + dy * dy);
+}
 
 // DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
 // Platform.reset (platform.py:104-114).  `episode` is the value after the
@@ -118,6 +127,7 @@ __device__ __forceinline__ void spawn(const DDConfig& c, int64_t env, Lane& s) {
     s.status = 0u;  // not done / landed / crashed; platform direction +1
     s.steps = 0;
     s.total = 0.0;
+    measure(s);
 }
 
 // physics.normalize_angle (physics.py:26-39).  From any state step() can
@@ -174,31 +184,30 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
     sincos(s.angle * kDeg2Rad, &sb, &cb);
     const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
     const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
-    const bool on_pad = (s.px - c.platform_half_width <= bx) && (bx <= s.px + c.platform_half_width) &&
-                        (s.py - c.platform_half_height <= by) && (by <= s.py + c.platform_half_height);
-    const double speed = sqrt(s.vx * s.vx + s.vy * s.vy);
-    const bool slow = !(speed > c.max_landing_velocity);
+    const bool on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
+                        (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
+    measure(s);  // speed (get_speed) and distance (physics.distance), shared with get_state
+    const bool slow = !(s.speed > c.max_landing_velocity);
     const bool upright = fabs(s.angle) <= c.max_landing_angle;
 
-    double reward = c.reward_step;
-    if (on_pad && slow && upright) {                      // _check_landing
-        s.status |= DD_ST_LANDED | DD_ST_DONE;
-        reward += c.reward_landing;
-    } else if (s.y > c.ground_level) {                    // _check_crash (landing ruled out)
-        s.status |= DD_ST_CRASHED | DD_ST_DONE;
-        reward += c.reward_crash;
-    } else if (s.fuel <= 0.0) {                           // out of fuel
-        s.status |= DD_ST_CRASHED | DD_ST_DONE;
-        reward += c.reward_out_of_fuel;
-    } else if (s.x < -c.oob_margin || s.x > c.world_width + c.oob_margin ||
-               s.y < -c.oob_margin || s.y > c.world_height + c.oob_margin) {
-        s.status |= DD_ST_CRASHED | DD_ST_DONE;
-        reward += c.reward_out_of_bounds;
-    } else {                                              // proximity shaping
-        const double dx = s.px - s.x, dy = s.py - s.y;
-        const double dist = sqrt(dx * dx + dy * dy);
-        reward += div_exact(c.shaping_offset - dist, c.shaping_scale, k.inv_shaping);
-    }
+    // _calculate_reward's cascade, evaluated branch-free: every predicate is
+    // formed, then the first that holds picks the term.  (The nested
+    // else-if form miscompiled on ROCm 7.2 / gfx950: the divergent-branch phi
+    // register of the out-of-bounds term was reused as a temporary, giving
+    // 649.9 instead of -50.1; tests/test_gpu_parity.py pins every branch.)
+    const bool landing = on_pad & slow & upright;                         // _check_landing
+    const bool crash = s.y > c.ground_level;                              // _check_crash, landing ruled out
+    const bool no_fuel = s.fuel <= 0.0;
+    const bool oob = (s.x < -c.oob_margin) | (s.x > c.world_width + c.oob_margin) |
+                     (s.y < -c.oob_margin) | (s.y > c.world_height + c.oob_margin);
+    double term = div_exact(c.shaping_offset - s.dist, c.shaping_scale, k.inv_shaping);
+    term = oob ? c.reward_out_of_bounds : term;
+    term = no_fuel ? c.reward_out_of_fuel : term;
+    term = crash ? c.reward_crash : term;
+    term = landing ? c.reward_landing : term;
+    const bool terminal = landing | crash | no_fuel | oob;
+    s.status |= landing ? (DD_ST_LANDED | DD_ST_DONE) : terminal ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
+    const double reward = c.reward_step + term;
     s.total += reward;
     s.steps += 1;
     return reward;
@@ -208,8 +217,7 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
 __device__ __forceinline__ void observe(const Consts& k, const Lane& s, float o[DD_OBS_DIM]) {
     const DDConfig& c = k.c;
     const double dx = s.px - s.x, dy = s.py - s.y;
-    const double dist = sqrt(dx * dx + dy * dy);
-    const double speed = sqrt(s.vx * s.vx + s.vy * s.vy);
+    const double dist = s.dist, speed = s.speed;  // measure() ran on this state
     o[0] = (float)div_exact(s.x, c.world_width, k.inv_w);
     o[1] = (float)div_exact(s.y, c.world_height, k.inv_h);
     o[2] = (float)div_exact(s.vx, c.vel_scale, k.inv_vel);
@@ -338,7 +346,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs p, Soa<T> a) {
                     s.episode = a.episode[i];
                     spawn(c, a.env_id_base + i, s);
                     store_spawn(a, i, s);
-                } // else sticky done (game_engine.py:107-111): nothing changes
+                } else {  // sticky done (game_engine.py:107-111): nothing changes
+                    measure(s);
+                }
             } else {
                 reward = frame(p.k, act, s);
                 ended = (s.status & DD_ST_DONE) != 0;
@@ -409,6 +419,7 @@ __global__ __launch_bounds__(kBlock) void obs_kernel(Consts k, Soa<T> a, float* 
             Lane s;
             load_dynamics(a, i, s);
             s.status = a.status[i];
+            measure(s);
             float o[DD_OBS_DIM];
             observe(k, s, o);
 #pragma unroll
