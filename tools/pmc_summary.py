@@ -1,0 +1,47 @@
+#!/usr/bin/env python
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the step kernel
+into profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+
+Per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KiB; on gfx950
+FETCH_SIZE counts each 128-B fabric read request as 64 B, so the read bytes
+are 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 are the written bytes.  The two
+counters come from separate passes (FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2).
+
+    python tools/pmc_summary.py OUT.json ENVS PRECISION OBS FETCH.csv WRITE.csv [...]
+"""
+import csv
+import json
+import sys
+
+
+def mean_counter(path, name):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if "step_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name]
+    if not vals:
+        raise SystemExit(f"no {name} rows for step_kernel in {path}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    out = sys.argv[1]
+    args = sys.argv[2:]
+    try:
+        doc = json.load(open(out))
+    except (OSError, ValueError):
+        doc = {"note": __doc__.strip().splitlines()[0], "rows": []}
+    for i in range(0, len(args), 5):
+        envs, prec, obs, fpath, wpath = args[i:i + 5]
+        fetch, nf = mean_counter(fpath, "FETCH_SIZE")
+        write, nw = mean_counter(wpath, "WRITE_SIZE")
+        row = {"envs": int(envs), "precision": prec, "obs": obs == "1",
+               "fetch_size_kib": round(fetch, 3), "write_size_kib": round(write, 3),
+               "read_bytes_per_launch": int(2 * fetch * 1024), "write_bytes_per_launch": int(write * 1024),
+               "hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024), "dispatches": [nf, nw],
+               "source": [fpath, wpath]}
+        doc["rows"] = [r for r in doc["rows"] if not (r["envs"] == row["envs"] and r["precision"] == prec
+                                                      and r["obs"] == row["obs"])] + [row]
+    json.dump(doc, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
