@@ -78,9 +78,11 @@ static void rotate_y(double y, double angle_deg, double *ox, double *oy) {
 }
 
 static double wrap_degrees(double a) {
-    int guard = 0; /* same finite bound as the kernel; unreachable from step() */
-    while (a > 180.0 && guard < 64) { a -= 360.0; ++guard; }
-    while (a < -180.0 && guard < 128) { a += 360.0; ++guard; }
+    /* physics.normalize_angle's loops.  Past |a| = 2^55, a - 360 == a and the
+     * reference never returns; the oracle reports NaN there instead of hanging. */
+    if (!(fabs(a) < 36028797018963968.0)) return fabs(a) < INFINITY ? NAN : a;
+    while (a > 180.0) a -= 360.0;
+    while (a < -180.0) a += 360.0;
     return a;
 }
 

@@ -17,14 +17,27 @@
 #include <stdint.h>
 
 #include "dronestep.h"
+#include "trig.h"
 
 namespace dd {
 
 constexpr int kBlock = 256;  // 4 waves; one obs tile = 256 rows
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kWave = 64;
 
 // numpy's deg2rad: x * (NPY_PI / 180.0)   (physics.py:16, np.radians)
 constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
+
+// sin and cos of an angle in degrees, as rotate_point computes them
+// (physics.py:16-18).  DD_TRIG_OCML selects the ROCm device library's
+// general-argument sincos instead of trig.h's (timing experiments).
+__device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
+#ifdef DD_TRIG_OCML
+    ::sincos(deg * kDeg2Rad, s, c);
+#else
+    trig::sincos(deg * kDeg2Rad, s, c);
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11).  Spawn draws are keyed by
@@ -74,16 +87,6 @@ inline Consts make_consts(const DDConfig& c) {
     return k;
 }
 
-// x / d, correctly rounded, in three double ops instead of the ~10 of the
-// general division sequence.  inv_d = RN(1/d); q0 = RN(x * inv_d) is faithful,
-// so by Markstein's theorem RN(q0 + RN(1/d) * (x - q0 * d)) = RN(x / d), the
-// reference's quotient, bit for bit (finite operands, no underflow).
-__device__ __forceinline__ double div_exact(double x, double d, double inv_d) {
-    const double q0 = x * inv_d;
-    const double r = fma(-q0, d, x);
-    return fma(r, inv_d, q0);
-}
-
 // The per-lane state, widened to double for the frame's arithmetic.
 struct Lane {
     double x, y, vx, vy, angle, omega, fuel, px, py, total;
@@ -130,16 +133,6 @@ __device__ __forceinline__ void spawn(const DDConfig& c, int64_t env, Lane& s) {
     measure(s);
 }
 
-// physics.normalize_angle (physics.py:26-39).  From any state step() can
-// reach, |omega| < 6 deg/frame, so the loops run at most once; the guard keeps
-// every wave finite for an arbitrary user-written angle.
-__device__ __forceinline__ double normalize_angle(double a) {
-    int guard = 0;
-    while (a > 180.0 && guard < 64) { a -= 360.0; ++guard; }
-    while (a < -180.0 && guard < 128) { a += 360.0; ++guard; }
-    return a;
-}
-
 // One frame of a live lane: Drone.apply_thrust (drone.py:44-76), wind
 // (game_engine.py:121-123), Drone.update (drone.py:78-103), Platform.update
 // (platform.py:31-49), _calculate_reward with _check_landing / _check_crash /
@@ -151,7 +144,7 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
     if (main_on && s.fuel > 0.0) {
         // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
         double sa, ca;
-        sincos(s.angle * kDeg2Rad, &sa, &ca);
+        sincos_deg(s.angle, &sa, &ca);
         const double ty = -c.main_thrust_power;
         s.vx += 0.0 * ca - ty * sa;
         s.vy += 0.0 * sa + ty * ca;
@@ -170,7 +163,7 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
     s.y += s.vy * c.dt;
     s.angle += s.omega * c.dt;
     s.omega *= c.angular_drag;
-    s.angle = normalize_angle(s.angle);
+    s.angle = trig::normalize_angle(s.angle);
 
     if (c.platform_moving) {
         const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
@@ -181,7 +174,7 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
 
     // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
     double sb, cb;
-    sincos(s.angle * kDeg2Rad, &sb, &cb);
+    sincos_deg(s.angle, &sb, &cb);
     const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
     const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
     const bool on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
@@ -200,7 +193,7 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
     const bool no_fuel = s.fuel <= 0.0;
     const bool oob = (s.x < -c.oob_margin) | (s.x > c.world_width + c.oob_margin) |
                      (s.y < -c.oob_margin) | (s.y > c.world_height + c.oob_margin);
-    double term = div_exact(c.shaping_offset - s.dist, c.shaping_scale, k.inv_shaping);
+    double term = trig::div_exact(c.shaping_offset - s.dist, c.shaping_scale, k.inv_shaping);
     term = oob ? c.reward_out_of_bounds : term;
     term = no_fuel ? c.reward_out_of_fuel : term;
     term = crash ? c.reward_crash : term;
@@ -214,23 +207,23 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
 }
 
 // DroneGame.get_state (game_engine.py:140-177) in state_to_array order.
-__device__ __forceinline__ void observe(const Consts& k, const Lane& s, float o[DD_OBS_DIM]) {
+__device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o) {
     const DDConfig& c = k.c;
     const double dx = s.px - s.x, dy = s.py - s.y;
     const double dist = s.dist, speed = s.speed;  // measure() ran on this state
-    o[0] = (float)div_exact(s.x, c.world_width, k.inv_w);
-    o[1] = (float)div_exact(s.y, c.world_height, k.inv_h);
-    o[2] = (float)div_exact(s.vx, c.vel_scale, k.inv_vel);
-    o[3] = (float)div_exact(s.vy, c.vel_scale, k.inv_vel);
-    o[4] = (float)div_exact(s.angle, c.angle_scale, k.inv_angle);
-    o[5] = (float)div_exact(s.omega, c.vel_scale, k.inv_vel);
-    o[6] = (float)div_exact(s.fuel, c.max_fuel, k.inv_fuel);
-    o[7] = (float)div_exact(s.px, c.world_width, k.inv_w);
-    o[8] = (float)div_exact(s.py, c.world_height, k.inv_h);
-    o[9] = (float)div_exact(dist, c.world_width, k.inv_w);
-    o[10] = (float)div_exact(dx, c.world_width, k.inv_w);
-    o[11] = (float)div_exact(dy, c.world_height, k.inv_h);
-    o[12] = (float)div_exact(speed, c.vel_scale, k.inv_vel);
+    o[0] = (float)trig::div_exact(s.x, c.world_width, k.inv_w);
+    o[1] = (float)trig::div_exact(s.y, c.world_height, k.inv_h);
+    o[2] = (float)trig::div_exact(s.vx, c.vel_scale, k.inv_vel);
+    o[3] = (float)trig::div_exact(s.vy, c.vel_scale, k.inv_vel);
+    o[4] = (float)trig::div_exact(s.angle, c.angle_scale, k.inv_angle);
+    o[5] = (float)trig::div_exact(s.omega, c.vel_scale, k.inv_vel);
+    o[6] = (float)trig::div_exact(s.fuel, c.max_fuel, k.inv_fuel);
+    o[7] = (float)trig::div_exact(s.px, c.world_width, k.inv_w);
+    o[8] = (float)trig::div_exact(s.py, c.world_height, k.inv_h);
+    o[9] = (float)trig::div_exact(dist, c.world_width, k.inv_w);
+    o[10] = (float)trig::div_exact(dx, c.world_width, k.inv_w);
+    o[11] = (float)trig::div_exact(dy, c.world_height, k.inv_h);
+    o[12] = (float)trig::div_exact(speed, c.vel_scale, k.inv_vel);
     o[13] = (s.status & DD_ST_LANDED) ? 1.0f : 0.0f;
     o[14] = (s.status & DD_ST_CRASHED) ? 1.0f : 0.0f;
 }
@@ -286,9 +279,13 @@ __device__ __forceinline__ void flush_obs_tile(const float* tile, float* obs, in
     const bool aligned = ((uintptr_t)dst & 15u) == 0;
     if (aligned) {
         const int nv = nf >> 2;
-        const float4* src4 = reinterpret_cast<const float4*>(tile);
-        float4* dst4 = reinterpret_cast<float4*>(dst);
+        const f32x4* src4 = reinterpret_cast<const f32x4*>(tile);
+        f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
+#ifdef DD_NT_OBS
+        for (int k = threadIdx.x; k < nv; k += kBlock) __builtin_nontemporal_store(src4[k], &dst4[k]);
+#else
         for (int k = threadIdx.x; k < nv; k += kBlock) dst4[k] = src4[k];
+#endif
         for (int k = (nv << 2) + threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
     } else {
         for (int k = threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
@@ -322,70 +319,72 @@ __device__ __forceinline__ uint32_t load_action(const void* actions, int64_t i) 
 // dd_step kernel.  One 256-lane tile per block.  (A grid-stride loop makes
 // hipcc hoist every kernarg constant out of the loop: 147 SGPR spills and 137
 // VGPRs against 0 and 74 for one tile per block.)
+#ifndef DD_STEP_MIN_WAVES
+#define DD_STEP_MIN_WAVES 1  // per SIMD; experiments raise it to force fewer VGPRs
+#endif
+
 template <typename T, int AFMT>
-__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs p, Soa<T> a) {
+__global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
     __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
     const DDConfig& c = p.k.c;
-    {
-        const int64_t t = blockIdx.x;
-        const int64_t i = t * kBlock + threadIdx.x;
-        const bool live = i < p.n;
-        bool ended = false;  // episode ended in this call (for compaction)
+    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
+    const int64_t i = row0 + threadIdx.x;
+    const bool live = i < p.n;
+    bool ended = false;  // episode ended in this call (for compaction)
+    if (live) {
         Lane s;
-        float o[DD_OBS_DIM];
-        if (live) {
-            load_dynamics(a, i, s);
-            s.status = a.status[i];
-            s.steps = a.steps[i];
-            s.total = a.total[i];
-            const uint32_t act = load_action<AFMT>(p.actions, i);
-            double reward;
-            if (s.status & DD_ST_DONE) {
-                reward = 0.0;
-                if (c.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
-                    s.episode = a.episode[i];
-                    spawn(c, a.env_id_base + i, s);
-                    store_spawn(a, i, s);
-                } else {  // sticky done (game_engine.py:107-111): nothing changes
-                    measure(s);
-                }
-            } else {
-                reward = frame(p.k, act, s);
-                ended = (s.status & DD_ST_DONE) != 0;
-                store_dynamics(a, i, s);
-                if (c.platform_moving) { a.px[i] = (T)s.px; a.status[i] = (uint8_t)s.status; }
-                else if (ended) a.status[i] = (uint8_t)s.status;
-                a.steps[i] = s.steps;
-                a.total[i] = (T)s.total;
+        load_dynamics(a, i, s);
+        s.status = a.status[i];
+        s.steps = a.steps[i];
+        s.total = a.total[i];
+        const uint32_t act = load_action<AFMT>(p.actions, i);
+        double reward;
+        if (s.status & DD_ST_DONE) {
+            reward = 0.0;
+            if (c.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
+                s.episode = a.episode[i];
+                spawn(c, a.env_id_base + i, s);
+                store_spawn(a, i, s);
+            } else {  // sticky done (game_engine.py:107-111): nothing changes
+                measure(s);
             }
-            static_cast<T*>(p.reward)[i] = (T)reward;
-            p.done[i] = (s.status & DD_ST_DONE) ? 1 : 0;
-            if (p.obs) observe(p.k, s, o);
+        } else {
+            reward = frame(p.k, act, s);
+            ended = (s.status & DD_ST_DONE) != 0;
+            store_dynamics(a, i, s);
+            if (c.platform_moving) { a.px[i] = (T)s.px; a.status[i] = (uint8_t)s.status; }
+            else if (ended) a.status[i] = (uint8_t)s.status;
+            a.steps[i] = s.steps;
+            a.total[i] = (T)s.total;
         }
-        if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
-            const uint64_t m = __ballot(ended);
-            if (m) {
-                const int lane = threadIdx.x & (kWave - 1);
-                const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                int base = 0;
-                if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(p.done_count, __popcll(m));
-                base = __shfl(base, __ffsll((unsigned long long)m) - 1);
-                if (ended) p.done_idx[base + before] = (int32_t)i;
-            }
-        }
-        if (p.obs) {  // uniform across the grid
-            if (live) {
-#pragma unroll
-                for (int k = 0; k < DD_OBS_DIM; ++k) tile[threadIdx.x * DD_OBS_DIM + k] = o[k];
-            }
-            __syncthreads();
-            const int64_t row0 = t * kBlock;
-            const int rows = (int)((p.n - row0) < kBlock ? (p.n - row0) : kBlock);
-            flush_obs_tile(tile, p.obs, row0, rows);
-            __syncthreads();
+        static_cast<T*>(p.reward)[i] = (T)reward;
+        p.done[i] = (s.status & DD_ST_DONE) ? 1 : 0;
+#ifdef DD_OBS_STRIDED
+        if (p.obs) observe(p.k, s, p.obs + i * DD_OBS_DIM);
+#else
+        if (p.obs) observe(p.k, s, tile + threadIdx.x * DD_OBS_DIM);  // row -> LDS (stride 15: no bank conflict)
+#endif
+    }
+    if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
+        const uint64_t m = __ballot(ended);
+        if (m) {
+            const int lane = threadIdx.x & (kWave - 1);
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.done_count, __popcll(m));
+            base = __shfl(base, leader);
+            if (ended) p.done_idx[base + before] = (int32_t)i;
         }
     }
+#ifndef DD_OBS_STRIDED
+    if (p.obs) {  // uniform across the grid: the tile leaves as 16-byte stores
+        __syncthreads();
+        const int rows = (int)((p.n - row0) < kBlock ? (p.n - row0) : kBlock);
+        flush_obs_tile(tile, p.obs, row0, rows);
+    }
+#endif
 }
 
 // dd_reset kernel: masked re-spawn (+ optional reset observation).
@@ -399,38 +398,25 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Consts k, Soa<T> a, const
     s.episode = a.episode[i];
     spawn(k.c, a.env_id_base + i, s);
     store_spawn(a, i, s);
-    if (obs) {
-        float o[DD_OBS_DIM];
-        observe(k, s, o);
-        float* row = obs + i * DD_OBS_DIM;
-#pragma unroll
-        for (int k = 0; k < DD_OBS_DIM; ++k) row[k] = o[k];
-    }
+    if (obs) observe(k, s, obs + i * DD_OBS_DIM);
 }
 
 // dd_write_obs kernel: observation of the current state, LDS-staged.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void obs_kernel(Consts k, Soa<T> a, float* obs, int64_t n) {
     __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
-    {
-        const int64_t t = blockIdx.x;
-        const int64_t i = t * kBlock + threadIdx.x;
-        if (i < n) {
-            Lane s;
-            load_dynamics(a, i, s);
-            s.status = a.status[i];
-            measure(s);
-            float o[DD_OBS_DIM];
-            observe(k, s, o);
-#pragma unroll
-            for (int k = 0; k < DD_OBS_DIM; ++k) tile[threadIdx.x * DD_OBS_DIM + k] = o[k];
-        }
-        __syncthreads();
-        const int64_t row0 = t * kBlock;
-        const int rows = (int)((n - row0) < kBlock ? (n - row0) : kBlock);
-        flush_obs_tile(tile, obs, row0, rows);
-        __syncthreads();
+    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
+    const int64_t i = row0 + threadIdx.x;
+    if (i < n) {
+        Lane s;
+        load_dynamics(a, i, s);
+        s.status = a.status[i];
+        measure(s);
+        observe(k, s, tile + threadIdx.x * DD_OBS_DIM);
     }
+    __syncthreads();
+    const int rows = (int)((n - row0) < kBlock ? (n - row0) : kBlock);
+    flush_obs_tile(tile, obs, row0, rows);
 }
 
 // dd_get_info kernel: pixel distance and speed (game_engine.py:292-296).

@@ -1,0 +1,119 @@
+// trig.h — double-precision angle math of the drone frame: sin/cos of the
+// rotation, exact division by the observation scales, angle wrapping.
+//
+// The frame takes sin/cos of angle * (pi/180) twice per drone (thrust vector
+// and bottom centre, physics.py:6-23).  Angles live in [-180, 180] degrees
+// (normalize_angle), so |x| <= pi + 1 ulp and the quadrant is |n| <= 2.  The
+// general OCML sincos spends ~100 VALU instructions on its fast path
+// (double-double Cody-Waite reduction sized for huge arguments); this one
+// spends ~40 for |x| < 2^19 * pi/2:
+//   * reduction: the classic two-round Cody-Waite split of pi/2 (33-bit head,
+//     so n * head is exact) good to ~118 bits, keeping the tail y1;
+//   * kernels: the public-domain fdlibm minimax polynomials (Sun, 1993) for
+//     sin and cos on [-pi/4, pi/4] with the tail correction; both are below
+//     1 ulp, the same accuracy class as glibc's correctly-rounded-in-practice
+//     sin/cos that the reference calls through numpy.
+// Beyond |x| = 2^19 * pi/2 (angles past 4.7e7 degrees, far outside anything
+// step() produces or the reference can normalise) the reduction loses
+// accuracy; no library fallback is compiled in, so the kernel carries no
+// Payne-Hanek code.  Compiled with -ffp-contract=off: every step below relies
+// on the separate roundings it is written with.
+#pragma once
+
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define DD_HD __host__ __device__
+#else
+#define DD_HD
+#endif
+
+namespace dd {
+namespace trig {
+
+constexpr double kInvPio2 = 6.36619772367581382433e-01;  // 0x3FE45F306DC9C883
+constexpr double kPio2_1 = 1.57079632673412561417e+00;   // 0x3FF921FB54400000 (33 bits)
+constexpr double kPio2_2 = 6.07710050630396597660e-11;   // 0x3DD0B4611A600000 (33 bits)
+constexpr double kPio2_2t = 2.02226624879595063154e-21;  // 0x3BA3198A2E037073
+
+constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+
+// sin(y0 + y1), |y0 + y1| <= pi/4, |y1| tiny
+DD_HD inline double ksin(double x, double y) {
+    const double z = x * x;
+    const double v = z * x;
+    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+
+// cos(y0 + y1), |y0 + y1| <= pi/4
+DD_HD inline double kcos(double x, double y) {
+    const double z = x * x;
+    const double w = z * z;
+    const double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    const double hz = 0.5 * z;
+    const double u = 1.0 - hz;
+    return u + (((1.0 - u) - hz) + (z * r - x * y));
+}
+
+// (sin x, cos x), accurate (< 1 ulp) for |x| < 2^19 * pi/2.
+DD_HD inline void sincos(double x, double* s, double* c) {
+    const double fn = rint(x * kInvPio2);
+    const int n = (int)fn;
+    const double t = x - fn * kPio2_1;  // exact: fn * head has <= 52 bits, Sterbenz
+    double w = fn * kPio2_2;            // exact (33-bit constant)
+    const double r = t - w;
+    w = fn * kPio2_2t - ((t - r) - w);
+    const double y0 = r - w;
+    const double y1 = (r - y0) - w;
+    const double sv = ksin(y0, y1);
+    const double cv = kcos(y0, y1);
+    switch (n & 3) {
+        case 0: *s = sv; *c = cv; break;
+        case 1: *s = cv; *c = -sv; break;
+        case 2: *s = -sv; *c = -cv; break;
+        default: *s = -cv; *c = sv; break;
+    }
+}
+
+// x / d, correctly rounded, in three double ops instead of the ~10 of the
+// general division sequence.  inv_d = RN(1/d); q0 = RN(x * inv_d) is a
+// faithful quotient, so by Markstein's theorem RN(q0 + inv_d * (x - q0 * d))
+// = RN(x / d): the reference's quotient, bit for bit (finite operands, no
+// underflow).  fma() is always fused, whatever -ffp-contract says.
+DD_HD inline double div_exact(double x, double d, double inv_d) {
+    const double q0 = x * inv_d;
+    const double r = fma(-q0, d, x);
+    return fma(r, inv_d, q0);
+}
+
+// physics.normalize_angle (physics.py:26-39) in O(1).  The reference's loops
+// subtract (add) 360 while the angle is > 180 (< -180).  For |a| < 2^55 each
+// a - 360 is exact (360 is a multiple of ulp(a)), so k passes of the loop
+// equal one exact a - k * 360; k comes from a division plus one correction
+// either way.  (Past 2^55 the reference's loop never terminates.)
+DD_HD inline double normalize_angle(double a) {
+    if (a > 180.0) {
+        const double k = ceil((a - 180.0) / 360.0);
+        double r = a - k * 360.0;
+        r = r > 180.0 ? r - 360.0 : r;    // k one short
+        r = r <= -180.0 ? r + 360.0 : r;  // k one past: the loop stops once r <= 180
+        return r;
+    }
+    if (a < -180.0) {
+        const double k = ceil((-180.0 - a) / 360.0);
+        double r = a + k * 360.0;
+        r = r < -180.0 ? r + 360.0 : r;
+        r = r >= 180.0 ? r - 360.0 : r;
+        return r;
+    }
+    return a;
+}
+
+}  // namespace trig
+}  // namespace dd

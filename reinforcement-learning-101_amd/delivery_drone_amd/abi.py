@@ -109,31 +109,34 @@ def library_path() -> str:
     return os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "libdronestep.so")
 
 
+def load(path: str) -> ctypes.CDLL:
+    """Load a build of the library at ``path`` and bind the header's signatures."""
+    if not os.path.exists(path):
+        raise NativeLibraryError(
+            f"HIP extension not built: {path} is missing. "
+            "Run `python -c 'import __graft_entry__ as g; g.build()'` from the repo root.")
+    try:
+        handle = ctypes.CDLL(path)
+    except OSError as exc:  # pragma: no cover - depends on the box
+        raise NativeLibraryError(f"cannot load {path}: {exc}") from exc
+    for name, (restype, argtypes) in EXPORTS.items():
+        fn = getattr(handle, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    if handle.dd_abi_version() != DD_ABI_VERSION:
+        raise NativeLibraryError(f"{path}: ABI version mismatch; rebuild it")
+    return handle
+
+
 def lib() -> ctypes.CDLL:
-    """Load ``libdronestep.so`` (built by ``__graft_entry__.build()``); raise if absent."""
+    """The product library ``_native/libdronestep.so`` (built by
+    ``__graft_entry__.build()``); raises if it is absent."""
     global _LIB
-    if _LIB is not None:
-        return _LIB
-    with _LOCK:
-        if _LIB is not None:
-            return _LIB
-        path = library_path()
-        if not os.path.exists(path):
-            raise NativeLibraryError(
-                f"HIP extension not built: {path} is missing. "
-                "Run `python -c 'import __graft_entry__ as g; g.build()'` from the repo root.")
-        try:
-            handle = ctypes.CDLL(path)
-        except OSError as exc:  # pragma: no cover - depends on the box
-            raise NativeLibraryError(f"cannot load {path}: {exc}") from exc
-        for name, (restype, argtypes) in EXPORTS.items():
-            fn = getattr(handle, name)
-            fn.restype = restype
-            fn.argtypes = argtypes
-        if handle.dd_abi_version() != DD_ABI_VERSION:
-            raise NativeLibraryError("libdronestep.so ABI version mismatch; rebuild it")
-        _LIB = handle
-        return _LIB
+    if _LIB is None:
+        with _LOCK:
+            if _LIB is None:
+                _LIB = load(library_path())
+    return _LIB
 
 
 def check(code: int, what: str) -> None:

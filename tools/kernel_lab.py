@@ -1,0 +1,81 @@
+#!/usr/bin/env python
+"""A/B timing of step-kernel builds, interleaved in one process.
+
+Each variant is a build of the same source with one -D switch
+(tools/build_variants.sh).  For every batch size, every variant gets its own
+VecDroneEnv (config-3 workload: random spawn, auto-reset, obs on), a captured
+hipGraph of G steps, and R interleaved rounds of replays timed with HIP events
+on the replay stream.  Prints one JSON line per (N, variant): median and min
+us/step and the algorithmic GB/s of the median.
+
+    python tools/kernel_lab.py --variants base,ocml --envs 262144,16777216
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
+
+import torch  # noqa: E402
+
+from delivery_drone_amd import EnvConfig, VecDroneEnv, abi  # noqa: E402
+
+LAB = os.path.join(REPO, "reinforcement-learning-101_amd", "delivery_drone_amd", "_native", "lab")
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--variants", default="base")
+    p.add_argument("--envs", default="262144,16777216")
+    p.add_argument("--graph-steps", type=int, default=20)
+    p.add_argument("--rounds", type=int, default=9)
+    p.add_argument("--precision", default="f32")
+    p.add_argument("--no-obs", action="store_true")
+    args = p.parse_args()
+    dev = torch.device("cuda", 0)
+    libs = {v: abi.load(os.path.join(LAB, f"lib_{v}.so")) for v in args.variants.split(",")}
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=0)
+    G = args.graph_steps
+    for n in [int(x) for x in args.envs.split(",")]:
+        rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
+        stream = torch.cuda.Stream(dev)
+        runs = {}
+        for name, lib in libs.items():
+            env = VecDroneEnv(n, device=dev, config=cfg, precision=args.precision, library=lib)
+            env.reset()
+            with torch.cuda.stream(stream):
+                for k in range(3):
+                    env.step(rows[k], write_obs=not args.no_obs)
+                torch.cuda.synchronize(dev)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=stream):
+                    for k in range(G):
+                        env.step(rows[k % 8], write_obs=not args.no_obs)
+                g.replay()
+            torch.cuda.synchronize(dev)
+            runs[name] = (env, g, [])
+        for _ in range(args.rounds):
+            for name, (env, g, times) in runs.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                with torch.cuda.stream(stream):
+                    e0.record(stream)
+                    g.replay()
+                    e1.record(stream)
+                torch.cuda.synchronize(dev)
+                times.append(e0.elapsed_time(e1) * 1e3 / G)
+        for name, (env, g, times) in runs.items():
+            med = statistics.median(times)
+            bpe = env.step_bytes_per_env(with_obs=not args.no_obs)
+            print(json.dumps({"envs": n, "variant": name, "us_per_step_median": round(med, 3),
+                              "us_per_step_min": round(min(times), 3),
+                              "gbs_median": round(bpe * n / (med * 1e-6) / 1e9, 1),
+                              "steps_per_s": round(n / (med * 1e-6), 1)}), flush=True)
+        del runs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
