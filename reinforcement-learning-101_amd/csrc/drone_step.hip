@@ -3,18 +3,24 @@
 // One lane = one drone.  The frame of DroneGame.step (reference
 // delivery_drone/game/game_engine.py:95-138) is evaluated in IEEE double in
 // registers, in the reference's operation order, and rounded once on store
-// (DD_F32) or not at all (DD_F64).  The path is HBM-bound (~1 flop/B), so the
-// kernel is shaped for bytes, not FLOPs: SoA dword loads/stores coalesced per
-// wave64, world constants in the kernarg segment (SGPRs, wave-uniform),
-// observation rows transposed through LDS so the [N,15] tile leaves as
-// contiguous 16-byte stores, and done-lane compaction by wave ballots with one
-// atomic per wave.
+// (DD_F32) or not at all (DD_F64).  The path moves ~147 B per drone-frame for
+// ~220 double ops, so the kernel is shaped for bytes and for VALU issue:
+//   * SoA dword loads/stores, coalesced per wave64, addressed as a wave-uniform
+//     SGPR base + one 32-bit lane offset (launches are chunked so offsets fit);
+//   * the reference's world constants (config.py) folded into the instruction
+//     stream when the run uses them (the usual case), kernarg otherwise;
+//   * observation rows staged through LDS so each [256, 15] tile leaves as
+//     contiguous 16-byte non-temporal stores;
+//   * done-lane compaction by wave ballots, one atomic per wave.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
 // (-ffp-contract=off keeps every a*b+c as the reference's two roundings.)
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <type_traits>
 
 #include "dronestep.h"
 #include "trig.h"
@@ -22,8 +28,10 @@
 namespace dd {
 
 constexpr int kBlock = 256;  // 4 waves; one obs tile = 256 rows
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kWave = 64;
+// Lanes per launch: keeps every byte offset (lane x 8 B) below 2^31.
+constexpr int64_t kChunk = int64_t(1) << 28;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // numpy's deg2rad: x * (NPY_PI / 180.0)   (physics.py:16, np.radians)
 constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
@@ -37,6 +45,103 @@ __device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
 #else
     trig::sincos(deg * kDeg2Rad, s, c);
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// World constants
+// ---------------------------------------------------------------------------
+// config.py:17-68 as a DDConfig (also what dd_config_default returns).
+constexpr DDConfig reference_config() {
+    DDConfig c{};
+    c.gravity = 0.3;
+    c.drag = 0.99;
+    c.angular_drag = 0.95;
+    c.main_thrust_power = 0.6;
+    c.side_thrust_power = 0.3;
+    c.fuel_main = 2.0;
+    c.fuel_side = 1.0;
+    c.max_fuel = 1000.0;
+    c.drone_half_height = 20 / 2.0;
+    c.dt = 1.0;
+    c.platform_half_width = 100 / 2.0;
+    c.platform_half_height = 20 / 2.0;
+    c.platform_speed = 1.0;
+    c.platform_min_x = 100 / 2;
+    c.platform_max_x = 800 - 100 / 2;
+    c.max_landing_velocity = 3.0;
+    c.max_landing_angle = 20.0;
+    c.world_width = 800;
+    c.world_height = 600;
+    c.oob_margin = 50;
+    c.ground_level = 600 - 50;
+    c.wind_x = 0.0;
+    c.wind_y = 0.0;
+    c.reward_step = -0.1;
+    c.reward_landing = 100.0;
+    c.reward_crash = -100.0;
+    c.reward_out_of_fuel = -50.0;
+    c.reward_out_of_bounds = -50.0;
+    c.shaping_offset = 500;
+    c.shaping_scale = 5000;
+    c.vel_scale = 10.0;
+    c.angle_scale = 180.0;
+    c.drone_start_x = 800 / 2;
+    c.drone_start_y = 100;
+    c.drone_x_min = 100;
+    c.drone_x_max = 700;
+    c.drone_y_min = 50;
+    c.drone_y_max = 250;
+    c.platform_start_x = 800 / 2;
+    c.platform_start_y = 600 - 100;
+    c.platform_x_lo = 100 / 2 + 50;
+    c.platform_x_hi = 800 - 100 / 2 - 50;
+    c.platform_y_lo = 100;
+    c.platform_y_hi = 550;
+    c.wind_enabled = 0;
+    c.platform_moving = 0;
+    c.randomize_drone = 0;
+    c.randomize_platform = 1;
+    c.auto_reset = 0;
+    c.seed = 0;
+    return c;
+}
+
+// The constants the frame reads: the config plus the correctly rounded
+// reciprocals of its divisors (for trig::div_exact).
+struct Consts {
+    DDConfig c;
+    double inv_w, inv_h, inv_vel, inv_angle, inv_fuel, inv_shaping;
+};
+
+constexpr Consts make_consts(const DDConfig& c) {
+    Consts k{};
+    k.c = c;
+    k.inv_w = 1.0 / c.world_width;
+    k.inv_h = 1.0 / c.world_height;
+    k.inv_vel = 1.0 / c.vel_scale;
+    k.inv_angle = 1.0 / c.angle_scale;
+    k.inv_fuel = 1.0 / c.max_fuel;
+    k.inv_shaping = 1.0 / c.shaping_scale;
+    return k;
+}
+
+// The reference's physics, reward and observation constants as compile-time
+// data: kernels instantiated with kRef = true read them from here and the
+// compiler folds them into the instruction stream (no kernarg SGPRs, no SGPR
+// spills).  Switches, spawn ranges, wind and seed always come from the call.
+__device__ constexpr Consts kRefConsts = make_consts(reference_config());
+
+// True when every double the frame reads (wind aside) equals config.py's.
+inline bool uses_reference_physics(const DDConfig& c) {
+    const DDConfig r = reference_config();
+    const double* a = &c.gravity;
+    const double* b = &r.gravity;
+    const int n = (int)((&c.vel_scale - &c.gravity) + 1);
+    for (int j = 0; j < n; ++j) {
+        if (a + j == &c.wind_x || a + j == &c.wind_y) continue;
+        if (memcmp(a + j, b + j, sizeof(double)) != 0) return false;
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -68,25 +173,9 @@ __device__ __forceinline__ int32_t draw_range(uint32_t r, int32_t lo, uint32_t s
     return lo + (int32_t)(((uint64_t)r * span) >> 32);
 }
 
-// World constants as the kernels see them: the public config plus the
-// correctly rounded reciprocals of the divisors, computed once on the host.
-struct Consts {
-    DDConfig c;
-    double inv_w, inv_h, inv_vel, inv_angle, inv_fuel, inv_shaping;
-};
-
-inline Consts make_consts(const DDConfig& c) {
-    Consts k;
-    k.c = c;
-    k.inv_w = 1.0 / c.world_width;
-    k.inv_h = 1.0 / c.world_height;
-    k.inv_vel = 1.0 / c.vel_scale;
-    k.inv_angle = 1.0 / c.angle_scale;
-    k.inv_fuel = 1.0 / c.max_fuel;
-    k.inv_shaping = 1.0 / c.shaping_scale;
-    return k;
-}
-
+// ---------------------------------------------------------------------------
+// One drone
+// ---------------------------------------------------------------------------
 // The per-lane state, widened to double for the frame's arithmetic.
 struct Lane {
     double x, y, vx, vy, angle, omega, fuel, px, py, total;
@@ -104,8 +193,8 @@ __device__ __forceinline__ void measure(Lane& s) {
 }
 
 // DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
-// Platform.reset (platform.py:104-114).  `episode` is the value after the
-// reset's `episode += 1`.
+// Platform.reset (platform.py:104-114).  `c` is the call's config (switches,
+// spawn ranges, seed); s.episode becomes the value after `episode += 1`.
 __device__ __forceinline__ void spawn(const DDConfig& c, int64_t env, Lane& s) {
     s.episode += 1;
     uint32_t r[4];
@@ -136,8 +225,10 @@ __device__ __forceinline__ void spawn(const DDConfig& c, int64_t env, Lane& s) {
 // One frame of a live lane: Drone.apply_thrust (drone.py:44-76), wind
 // (game_engine.py:121-123), Drone.update (drone.py:78-103), Platform.update
 // (platform.py:31-49), _calculate_reward with _check_landing / _check_crash /
-// _check_out_of_bounds (game_engine.py:179-279).  Returns the reward.
-__device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) {
+// _check_out_of_bounds (game_engine.py:179-279).  `k` holds the physics
+// (compile-time in the reference instantiation), `sw` the call's switches.
+// Returns the reward.
+__device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
     const DDConfig& c = k.c;
     const bool main_on = act & 1u, left_on = act & 2u, right_on = act & 4u;
 
@@ -154,7 +245,7 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
     if (right_on && s.fuel > 0.0) { s.omega += c.side_thrust_power; s.fuel -= c.fuel_side; }
     s.fuel = s.fuel > 0.0 ? s.fuel : 0.0;  // max(0, fuel)
 
-    if (c.wind_enabled) { s.vx += c.wind_x; s.vy += c.wind_y; }
+    if (sw.wind_enabled) { s.vx += sw.wind_x; s.vy += sw.wind_y; }
 
     s.vy += c.gravity * c.dt;
     s.vx *= c.drag;
@@ -165,7 +256,7 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
     s.omega *= c.angular_drag;
     s.angle = trig::normalize_angle(s.angle);
 
-    if (c.platform_moving) {
+    if (sw.platform_moving) {
         const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
         s.px += c.platform_speed * dir * c.dt;
         if (s.px <= c.platform_min_x) { s.px = c.platform_min_x; s.status &= ~DD_ST_PLAT_LEFT; }
@@ -206,11 +297,11 @@ __device__ __forceinline__ double frame(const Consts& k, uint32_t act, Lane& s) 
     return reward;
 }
 
-// DroneGame.get_state (game_engine.py:140-177) in state_to_array order.
+// DroneGame.get_state (game_engine.py:140-177) in state_to_array order;
+// measure() has run on `s`.
 __device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o) {
     const DDConfig& c = k.c;
     const double dx = s.px - s.x, dy = s.py - s.y;
-    const double dist = s.dist, speed = s.speed;  // measure() ran on this state
     o[0] = (float)trig::div_exact(s.x, c.world_width, k.inv_w);
     o[1] = (float)trig::div_exact(s.y, c.world_height, k.inv_h);
     o[2] = (float)trig::div_exact(s.vx, c.vel_scale, k.inv_vel);
@@ -220,14 +311,18 @@ __device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o
     o[6] = (float)trig::div_exact(s.fuel, c.max_fuel, k.inv_fuel);
     o[7] = (float)trig::div_exact(s.px, c.world_width, k.inv_w);
     o[8] = (float)trig::div_exact(s.py, c.world_height, k.inv_h);
-    o[9] = (float)trig::div_exact(dist, c.world_width, k.inv_w);
+    o[9] = (float)trig::div_exact(s.dist, c.world_width, k.inv_w);
     o[10] = (float)trig::div_exact(dx, c.world_width, k.inv_w);
     o[11] = (float)trig::div_exact(dy, c.world_height, k.inv_h);
-    o[12] = (float)trig::div_exact(speed, c.vel_scale, k.inv_vel);
+    o[12] = (float)trig::div_exact(s.speed, c.vel_scale, k.inv_vel);
     o[13] = (s.status & DD_ST_LANDED) ? 1.0f : 0.0f;
     o[14] = (s.status & DD_ST_CRASHED) ? 1.0f : 0.0f;
 }
 
+// ---------------------------------------------------------------------------
+// SoA access: wave-uniform base pointers (SGPRs) + one 32-bit byte offset per
+// lane, so every load/store is `global_load_dword v, v_off, s[base]`.
+// ---------------------------------------------------------------------------
 template <typename T>
 struct Soa {
     T *x, *y, *vx, *vy, *angle, *omega, *fuel, *px, *py, *total;
@@ -237,133 +332,139 @@ struct Soa {
 };
 
 template <typename T>
-__host__ Soa<T> soa_of(const DDState& st) {
+Soa<T> soa_of(const DDState& st, int64_t first) {
     Soa<T> s;
-    s.x = (T*)st.x; s.y = (T*)st.y; s.vx = (T*)st.vx; s.vy = (T*)st.vy;
-    s.angle = (T*)st.angle; s.omega = (T*)st.omega; s.fuel = (T*)st.fuel;
-    s.px = (T*)st.px; s.py = (T*)st.py; s.total = (T*)st.total_reward;
-    s.status = st.status; s.steps = st.steps; s.episode = st.episode;
-    s.env_id_base = st.env_id_base;
+    s.x = (T*)st.x + first; s.y = (T*)st.y + first; s.vx = (T*)st.vx + first; s.vy = (T*)st.vy + first;
+    s.angle = (T*)st.angle + first; s.omega = (T*)st.omega + first; s.fuel = (T*)st.fuel + first;
+    s.px = (T*)st.px + first; s.py = (T*)st.py + first; s.total = (T*)st.total_reward + first;
+    s.status = st.status + first; s.steps = st.steps + first; s.episode = st.episode + first;
+    s.env_id_base = st.env_id_base + first;
     return s;
 }
 
-template <typename T>
-__device__ __forceinline__ void load_dynamics(const Soa<T>& a, int64_t i, Lane& s) {
-    s.x = a.x[i]; s.y = a.y[i]; s.vx = a.vx[i]; s.vy = a.vy[i];
-    s.angle = a.angle[i]; s.omega = a.omega[i]; s.fuel = a.fuel[i];
-    s.px = a.px[i]; s.py = a.py[i];
+// element i of a lane array (i < kChunk)
+template <typename E>
+__device__ __forceinline__ E& at(E* base, uint32_t i) {
+    using B = typename std::conditional<std::is_const<E>::value, const char, char>::type;
+    return *reinterpret_cast<E*>(reinterpret_cast<B*>(base) + (uint32_t)(i * (uint32_t)sizeof(E)));
 }
 
 template <typename T>
-__device__ __forceinline__ void store_dynamics(const Soa<T>& a, int64_t i, const Lane& s) {
-    a.x[i] = (T)s.x; a.y[i] = (T)s.y; a.vx[i] = (T)s.vx; a.vy[i] = (T)s.vy;
-    a.angle[i] = (T)s.angle; a.omega[i] = (T)s.omega; a.fuel[i] = (T)s.fuel;
+__device__ __forceinline__ void load_dynamics(const Soa<T>& a, uint32_t i, Lane& s) {
+    s.x = at(a.x, i); s.y = at(a.y, i); s.vx = at(a.vx, i); s.vy = at(a.vy, i);
+    s.angle = at(a.angle, i); s.omega = at(a.omega, i); s.fuel = at(a.fuel, i);
+    s.px = at(a.px, i); s.py = at(a.py, i);
 }
 
 template <typename T>
-__device__ __forceinline__ void store_spawn(const Soa<T>& a, int64_t i, const Lane& s) {
+__device__ __forceinline__ void store_dynamics(const Soa<T>& a, uint32_t i, const Lane& s) {
+    at(a.x, i) = (T)s.x; at(a.y, i) = (T)s.y; at(a.vx, i) = (T)s.vx; at(a.vy, i) = (T)s.vy;
+    at(a.angle, i) = (T)s.angle; at(a.omega, i) = (T)s.omega; at(a.fuel, i) = (T)s.fuel;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_spawn(const Soa<T>& a, uint32_t i, const Lane& s) {
     store_dynamics(a, i, s);
-    a.px[i] = (T)s.px; a.py[i] = (T)s.py;
-    a.total[i] = (T)s.total;
-    a.status[i] = (uint8_t)s.status;
-    a.steps[i] = s.steps;
-    a.episode[i] = s.episode;
+    at(a.px, i) = (T)s.px; at(a.py, i) = (T)s.py;
+    at(a.total, i) = (T)s.total;
+    at(a.status, i) = (uint8_t)s.status;
+    at(a.steps, i) = s.steps;
+    at(a.episode, i) = s.episode;
 }
 
-// Writes the block's [rows, 15] observation tile from LDS to global memory as
-// 16-byte stores.  `tile` holds rows * 15 floats; obs_row0 = first row.
-__device__ __forceinline__ void flush_obs_tile(const float* tile, float* obs, int64_t row0, int rows) {
-    float* dst = obs + row0 * DD_OBS_DIM;
+// Writes a block's [rows, 15] observation tile from LDS to global memory as
+// 16-byte stores (non-temporal: the rows are the step's output stream, read
+// by the consumer, not by this kernel again).  dst = first row of the tile.
+__device__ __forceinline__ void flush_obs_tile(const float* tile, float* dst, int rows) {
     const int nf = rows * DD_OBS_DIM;
-    // row0 is a multiple of kBlock, so dst is 16-byte aligned whenever obs is.
-    const bool aligned = ((uintptr_t)dst & 15u) == 0;
-    if (aligned) {
+    // tiles start at multiples of 256 rows (15360 B): dst is 16-B aligned iff obs is
+    if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
         const int nv = nf >> 2;
         const f32x4* src4 = reinterpret_cast<const f32x4*>(tile);
         f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
-#ifdef DD_NT_OBS
-        for (int k = threadIdx.x; k < nv; k += kBlock) __builtin_nontemporal_store(src4[k], &dst4[k]);
+        for (int k = threadIdx.x; k < nv; k += kBlock) {
+#ifdef DD_PLAIN_OBS_STORES
+            dst4[k] = src4[k];
 #else
-        for (int k = threadIdx.x; k < nv; k += kBlock) dst4[k] = src4[k];
+            __builtin_nontemporal_store(src4[k], &dst4[k]);
 #endif
+        }
         for (int k = (nv << 2) + threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
     } else {
         for (int k = threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
     }
 }
 
+template <int AFMT>
+__device__ __forceinline__ uint32_t load_action(const void* actions, uint32_t i) {
+    if constexpr (AFMT == DD_ACT_BITMASK) {
+        return at(static_cast<const uint8_t*>(actions), i);
+    } else if constexpr (AFMT == DD_ACT_F32X3) {
+        const float* a = &at(static_cast<const float*>(actions), 3 * i);
+        return (a[0] != 0.0f ? 1u : 0u) | (a[1] != 0.0f ? 2u : 0u) | (a[2] != 0.0f ? 4u : 0u);
+    } else {
+        const uint8_t* a = &at(static_cast<const uint8_t*>(actions), 3 * i);
+        return (a[0] ? 1u : 0u) | (a[1] ? 2u : 0u) | (a[2] ? 4u : 0u);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// dd_step kernel: one 256-lane tile per block, one chunk of lanes per launch.
+// ---------------------------------------------------------------------------
 struct StepArgs {
-    Consts k;
-    const void* actions;
+    Consts k;              // runtime constants (switches, spawn; physics when !kRef)
+    const void* actions;   // chunk-relative
     void* reward;
     uint8_t* done;
     float* obs;
     int32_t* done_idx;
     int32_t* done_count;
-    int64_t n;
+    int32_t n;             // lanes in this chunk
+    int32_t idx_base;      // chunk start, for done_idx entries
 };
 
-template <int AFMT>
-__device__ __forceinline__ uint32_t load_action(const void* actions, int64_t i) {
-    if constexpr (AFMT == DD_ACT_BITMASK) {
-        return static_cast<const uint8_t*>(actions)[i];
-    } else if constexpr (AFMT == DD_ACT_F32X3) {
-        const float* a = static_cast<const float*>(actions) + 3 * i;
-        return (a[0] != 0.0f ? 1u : 0u) | (a[1] != 0.0f ? 2u : 0u) | (a[2] != 0.0f ? 4u : 0u);
-    } else {
-        const uint8_t* a = static_cast<const uint8_t*>(actions) + 3 * i;
-        return (a[0] ? 1u : 0u) | (a[1] ? 2u : 0u) | (a[2] ? 4u : 0u);
-    }
-}
-
-// dd_step kernel.  One 256-lane tile per block.  (A grid-stride loop makes
-// hipcc hoist every kernarg constant out of the loop: 147 SGPR spills and 137
-// VGPRs against 0 and 74 for one tile per block.)
 #ifndef DD_STEP_MIN_WAVES
 #define DD_STEP_MIN_WAVES 1  // per SIMD; experiments raise it to force fewer VGPRs
 #endif
 
-template <typename T, int AFMT>
+template <typename T, int AFMT, bool kRef>
 __global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
     __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
-    const DDConfig& c = p.k.c;
-    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
-    const int64_t i = row0 + threadIdx.x;
-    const bool live = i < p.n;
+    const DDConfig& sw = p.k.c;
+    const Consts& k = kRef ? kRefConsts : p.k;
+    const uint32_t row0 = blockIdx.x * kBlock;
+    const uint32_t i = row0 + threadIdx.x;
+    const bool live = i < (uint32_t)p.n;
     bool ended = false;  // episode ended in this call (for compaction)
     if (live) {
         Lane s;
         load_dynamics(a, i, s);
-        s.status = a.status[i];
-        s.steps = a.steps[i];
-        s.total = a.total[i];
+        s.status = at(a.status, i);
+        s.steps = at(a.steps, i);
+        s.total = at(a.total, i);
         const uint32_t act = load_action<AFMT>(p.actions, i);
         double reward;
         if (s.status & DD_ST_DONE) {
             reward = 0.0;
-            if (c.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
-                s.episode = a.episode[i];
-                spawn(c, a.env_id_base + i, s);
+            if (sw.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
+                s.episode = at(a.episode, i);
+                spawn(sw, a.env_id_base + i, s);
                 store_spawn(a, i, s);
             } else {  // sticky done (game_engine.py:107-111): nothing changes
                 measure(s);
             }
         } else {
-            reward = frame(p.k, act, s);
+            reward = frame(k, sw, act, s);
             ended = (s.status & DD_ST_DONE) != 0;
             store_dynamics(a, i, s);
-            if (c.platform_moving) { a.px[i] = (T)s.px; a.status[i] = (uint8_t)s.status; }
-            else if (ended) a.status[i] = (uint8_t)s.status;
-            a.steps[i] = s.steps;
-            a.total[i] = (T)s.total;
+            if (sw.platform_moving) { at(a.px, i) = (T)s.px; at(a.status, i) = (uint8_t)s.status; }
+            else if (ended) at(a.status, i) = (uint8_t)s.status;
+            at(a.steps, i) = s.steps;
+            at(a.total, i) = (T)s.total;
         }
-        static_cast<T*>(p.reward)[i] = (T)reward;
-        p.done[i] = (s.status & DD_ST_DONE) ? 1 : 0;
-#ifdef DD_OBS_STRIDED
-        if (p.obs) observe(p.k, s, p.obs + i * DD_OBS_DIM);
-#else
-        if (p.obs) observe(p.k, s, tile + threadIdx.x * DD_OBS_DIM);  // row -> LDS (stride 15: no bank conflict)
-#endif
+        at(static_cast<T*>(p.reward), i) = (T)reward;
+        at(p.done, i) = (s.status & DD_ST_DONE) ? 1 : 0;
+        if (p.obs) observe(k, s, tile + threadIdx.x * DD_OBS_DIM);  // row -> LDS (stride 15: no bank conflict)
     }
     if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
         const uint64_t m = __ballot(ended);
@@ -375,59 +476,57 @@ __global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArg
             int base = 0;
             if (lane == leader) base = atomicAdd(p.done_count, __popcll(m));
             base = __shfl(base, leader);
-            if (ended) p.done_idx[base + before] = (int32_t)i;
+            if (ended) p.done_idx[base + before] = p.idx_base + (int32_t)i;
         }
     }
-#ifndef DD_OBS_STRIDED
     if (p.obs) {  // uniform across the grid: the tile leaves as 16-byte stores
         __syncthreads();
-        const int rows = (int)((p.n - row0) < kBlock ? (p.n - row0) : kBlock);
-        flush_obs_tile(tile, p.obs, row0, rows);
+        const int rows = (int)min((uint32_t)kBlock, (uint32_t)p.n - row0);
+        flush_obs_tile(tile, p.obs + (size_t)row0 * DD_OBS_DIM, rows);
     }
-#endif
 }
 
 // dd_reset kernel: masked re-spawn (+ optional reset observation).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void reset_kernel(Consts k, Soa<T> a, const uint8_t* mask,
-                                                       float* obs, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    if (mask && !mask[i]) return;
+                                                       float* obs, int32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (uint32_t)n) return;
+    if (mask && !at(mask, i)) return;
     Lane s;
-    s.episode = a.episode[i];
+    s.episode = at(a.episode, i);
     spawn(k.c, a.env_id_base + i, s);
     store_spawn(a, i, s);
-    if (obs) observe(k, s, obs + i * DD_OBS_DIM);
+    if (obs) observe(k, s, obs + (size_t)i * DD_OBS_DIM);
 }
 
 // dd_write_obs kernel: observation of the current state, LDS-staged.
 template <typename T>
-__global__ __launch_bounds__(kBlock) void obs_kernel(Consts k, Soa<T> a, float* obs, int64_t n) {
+__global__ __launch_bounds__(kBlock) void obs_kernel(Consts k, Soa<T> a, float* obs, int32_t n) {
     __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
-    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
-    const int64_t i = row0 + threadIdx.x;
-    if (i < n) {
+    const uint32_t row0 = blockIdx.x * kBlock;
+    const uint32_t i = row0 + threadIdx.x;
+    if (i < (uint32_t)n) {
         Lane s;
         load_dynamics(a, i, s);
-        s.status = a.status[i];
+        s.status = at(a.status, i);
         measure(s);
         observe(k, s, tile + threadIdx.x * DD_OBS_DIM);
     }
     __syncthreads();
-    const int rows = (int)((n - row0) < kBlock ? (n - row0) : kBlock);
-    flush_obs_tile(tile, obs, row0, rows);
+    const int rows = (int)min((uint32_t)kBlock, (uint32_t)n - row0);
+    flush_obs_tile(tile, obs + (size_t)row0 * DD_OBS_DIM, rows);
 }
 
 // dd_get_info kernel: pixel distance and speed (game_engine.py:292-296).
 template <typename T>
-__global__ __launch_bounds__(kBlock) void info_kernel(Soa<T> a, T* distance, T* speed, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const double x = a.x[i], y = a.y[i], vx = a.vx[i], vy = a.vy[i];
-    const double dx = (double)a.px[i] - x, dy = (double)a.py[i] - y;
-    if (distance) distance[i] = (T)sqrt(dx * dx + dy * dy);
-    if (speed) speed[i] = (T)sqrt(vx * vx + vy * vy);
+__global__ __launch_bounds__(kBlock) void info_kernel(Soa<T> a, T* distance, T* speed, int32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (uint32_t)n) return;
+    const double x = at(a.x, i), y = at(a.y, i), vx = at(a.vx, i), vy = at(a.vy, i);
+    const double dx = (double)at(a.px, i) - x, dy = (double)at(a.py, i) - y;
+    if (distance) at(distance, i) = (T)sqrt(dx * dx + dy * dy);
+    if (speed) at(speed, i) = (T)sqrt(vx * vx + vy * vy);
 }
 
 // ---------------------------------------------------------------------------
@@ -500,11 +599,9 @@ __global__ __launch_bounds__(kBlock) void compact_scatter_kernel(const uint8_t* 
 }
 
 // ---------------------------------------------------------------------------
-// Host side: argument checks and launches.
+// Host side: argument checks, chunking and launches.
 // ---------------------------------------------------------------------------
 inline int64_t tiles_of(int64_t n) { return (n + kBlock - 1) / kBlock; }
-
-inline unsigned grid_of(int64_t n) { return (unsigned)tiles_of(n); }
 
 bool state_ok(const DDState* st) {
     return st && st->x && st->y && st->vx && st->vy && st->angle && st->omega && st->fuel && st->px &&
@@ -512,82 +609,46 @@ bool state_ok(const DDState* st) {
            (st->precision == DD_F32 || st->precision == DD_F64);
 }
 
-template <typename T, int AFMT>
-void launch_step(const StepArgs& p, const DDState& st, hipStream_t s) {
-    hipLaunchKernelGGL((step_kernel<T, AFMT>), dim3(grid_of(p.n)), dim3(kBlock), 0, s, p, soa_of<T>(st));
+template <typename T, int AFMT, bool kRef>
+void launch_step(const StepArgs& p, const Soa<T>& a, hipStream_t s) {
+    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
 }
 
-template <typename T>
-void launch_step_t(const StepArgs& p, int afmt, const DDState& st, hipStream_t s) {
+template <typename T, bool kRef>
+void launch_step_fmt(const StepArgs& p, int afmt, const Soa<T>& a, hipStream_t s) {
     switch (afmt) {
-        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK>(p, st, s); break;
-        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3>(p, st, s); break;
-        default: launch_step<T, DD_ACT_U8X3>(p, st, s); break;
+        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK, kRef>(p, a, s); break;
+        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3, kRef>(p, a, s); break;
+        default: launch_step<T, DD_ACT_U8X3, kRef>(p, a, s); break;
     }
 }
 
-int finish() {
-    const hipError_t e = hipGetLastError();
-    return (int)e;
+template <typename T>
+void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, hipStream_t s) {
+    const bool ref = uses_reference_physics(p.k.c);
+    const int64_t act_w = io.action_format == DD_ACT_F32X3 ? 12 : io.action_format == DD_ACT_U8X3 ? 3 : 1;
+    for (int64_t first = 0; first < n; first += kChunk) {
+        const int64_t len = n - first < kChunk ? n - first : kChunk;
+        p.actions = static_cast<const char*>(io.actions) + first * act_w;
+        p.reward = static_cast<T*>(io.reward) + first;
+        p.done = io.done + first;
+        p.obs = io.obs ? io.obs + first * DD_OBS_DIM : nullptr;
+        p.n = (int32_t)len;
+        p.idx_base = (int32_t)first;
+        const Soa<T> a = soa_of<T>(st, first);
+        if (ref) launch_step_fmt<T, true>(p, io.action_format, a, s);
+        else launch_step_fmt<T, false>(p, io.action_format, a, s);
+    }
 }
+
+int finish() { return (int)hipGetLastError(); }
 
 }  // namespace dd
 
 extern "C" {
 
 void dd_config_default(DDConfig* c) {
-    if (!c) return;
-    *c = DDConfig{};
-    c->gravity = 0.3;
-    c->drag = 0.99;
-    c->angular_drag = 0.95;
-    c->main_thrust_power = 0.6;
-    c->side_thrust_power = 0.3;
-    c->fuel_main = 2.0;
-    c->fuel_side = 1.0;
-    c->max_fuel = 1000.0;
-    c->drone_half_height = 20 / 2.0;
-    c->dt = 1.0;
-    c->platform_half_width = 100 / 2.0;
-    c->platform_half_height = 20 / 2.0;
-    c->platform_speed = 1.0;
-    c->platform_min_x = 100 / 2;
-    c->platform_max_x = 800 - 100 / 2;
-    c->max_landing_velocity = 3.0;
-    c->max_landing_angle = 20.0;
-    c->world_width = 800;
-    c->world_height = 600;
-    c->oob_margin = 50;
-    c->ground_level = 600 - 50;
-    c->wind_x = 0.0;
-    c->wind_y = 0.0;
-    c->reward_step = -0.1;
-    c->reward_landing = 100.0;
-    c->reward_crash = -100.0;
-    c->reward_out_of_fuel = -50.0;
-    c->reward_out_of_bounds = -50.0;
-    c->shaping_offset = 500;
-    c->shaping_scale = 5000;
-    c->vel_scale = 10.0;
-    c->angle_scale = 180.0;
-    c->drone_start_x = 800 / 2;
-    c->drone_start_y = 100;
-    c->drone_x_min = 100;
-    c->drone_x_max = 700;
-    c->drone_y_min = 50;
-    c->drone_y_max = 250;
-    c->platform_start_x = 800 / 2;
-    c->platform_start_y = 600 - 100;
-    c->platform_x_lo = 100 / 2 + 50;
-    c->platform_x_hi = 800 - 100 / 2 - 50;
-    c->platform_y_lo = 100;
-    c->platform_y_hi = 550;
-    c->wind_enabled = 0;
-    c->platform_moving = 0;
-    c->randomize_drone = 0;
-    c->randomize_platform = 1;
-    c->auto_reset = 0;
-    c->seed = 0;
+    if (c) *c = dd::reference_config();
 }
 
 int dd_step(const DDConfig* cfg, const DDState* st, const DDStepIO* io, int64_t n, void* stream) {
@@ -602,17 +663,12 @@ int dd_step(const DDConfig* cfg, const DDState* st, const DDStepIO* io, int64_t 
     }
     if (n == 0) return 0;  // empty batch: pointers may be null
     if (!dd::state_ok(st) || !io->actions || !io->reward || !io->done) return hipErrorInvalidValue;
-    dd::StepArgs p;
+    dd::StepArgs p{};
     p.k = dd::make_consts(*cfg);
-    p.actions = io->actions;
-    p.reward = io->reward;
-    p.done = io->done;
-    p.obs = io->obs;
     p.done_idx = io->done_idx;
     p.done_count = io->done_count;
-    p.n = n;
-    if (st->precision == DD_F32) dd::launch_step_t<float>(p, io->action_format, *st, s);
-    else dd::launch_step_t<double>(p, io->action_format, *st, s);
+    if (st->precision == DD_F32) dd::step_chunks<float>(p, *st, *io, n, s);
+    else dd::step_chunks<double>(p, *st, *io, n, s);
     return dd::finish();
 }
 
@@ -621,11 +677,17 @@ int dd_reset(const DDConfig* cfg, const DDState* st, const uint8_t* mask, float*
     if (n == 0) return 0;
     if (!dd::state_ok(st)) return hipErrorInvalidValue;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 g((unsigned)dd::tiles_of(n)), b(dd::kBlock);
-    if (st->precision == DD_F32)
-        hipLaunchKernelGGL(dd::reset_kernel<float>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<float>(*st), mask, obs, n);
-    else
-        hipLaunchKernelGGL(dd::reset_kernel<double>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<double>(*st), mask, obs, n);
+    const dd::Consts k = dd::make_consts(*cfg);
+    for (int64_t first = 0; first < n; first += dd::kChunk) {
+        const int32_t len = (int32_t)(n - first < dd::kChunk ? n - first : dd::kChunk);
+        const dim3 g((unsigned)dd::tiles_of(len)), b(dd::kBlock);
+        const uint8_t* m = mask ? mask + first : nullptr;
+        float* o = obs ? obs + first * DD_OBS_DIM : nullptr;
+        if (st->precision == DD_F32)
+            hipLaunchKernelGGL(dd::reset_kernel<float>, g, b, 0, s, k, dd::soa_of<float>(*st, first), m, o, len);
+        else
+            hipLaunchKernelGGL(dd::reset_kernel<double>, g, b, 0, s, k, dd::soa_of<double>(*st, first), m, o, len);
+    }
     return dd::finish();
 }
 
@@ -634,11 +696,16 @@ int dd_write_obs(const DDConfig* cfg, const DDState* st, float* obs, int64_t n, 
     if (n == 0) return 0;
     if (!obs || !dd::state_ok(st)) return hipErrorInvalidValue;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 g(dd::grid_of(n)), b(dd::kBlock);
-    if (st->precision == DD_F32)
-        hipLaunchKernelGGL(dd::obs_kernel<float>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<float>(*st), obs, n);
-    else
-        hipLaunchKernelGGL(dd::obs_kernel<double>, g, b, 0, s, dd::make_consts(*cfg), dd::soa_of<double>(*st), obs, n);
+    const dd::Consts k = dd::make_consts(*cfg);
+    for (int64_t first = 0; first < n; first += dd::kChunk) {
+        const int32_t len = (int32_t)(n - first < dd::kChunk ? n - first : dd::kChunk);
+        const dim3 g((unsigned)dd::tiles_of(len)), b(dd::kBlock);
+        float* o = obs + first * DD_OBS_DIM;
+        if (st->precision == DD_F32)
+            hipLaunchKernelGGL(dd::obs_kernel<float>, g, b, 0, s, k, dd::soa_of<float>(*st, first), o, len);
+        else
+            hipLaunchKernelGGL(dd::obs_kernel<double>, g, b, 0, s, k, dd::soa_of<double>(*st, first), o, len);
+    }
     return dd::finish();
 }
 
@@ -647,13 +714,18 @@ int dd_get_info(const DDConfig* cfg, const DDState* st, void* distance, void* sp
     if (n == 0 || (!distance && !speed)) return 0;
     if (!dd::state_ok(st)) return hipErrorInvalidValue;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 g((unsigned)dd::tiles_of(n)), b(dd::kBlock);
-    if (st->precision == DD_F32)
-        hipLaunchKernelGGL(dd::info_kernel<float>, g, b, 0, s, dd::soa_of<float>(*st), (float*)distance,
-                           (float*)speed, n);
-    else
-        hipLaunchKernelGGL(dd::info_kernel<double>, g, b, 0, s, dd::soa_of<double>(*st), (double*)distance,
-                           (double*)speed, n);
+    for (int64_t first = 0; first < n; first += dd::kChunk) {
+        const int32_t len = (int32_t)(n - first < dd::kChunk ? n - first : dd::kChunk);
+        const dim3 g((unsigned)dd::tiles_of(len)), b(dd::kBlock);
+        if (st->precision == DD_F32)
+            hipLaunchKernelGGL(dd::info_kernel<float>, g, b, 0, s, dd::soa_of<float>(*st, first),
+                               distance ? (float*)distance + first : nullptr,
+                               speed ? (float*)speed + first : nullptr, len);
+        else
+            hipLaunchKernelGGL(dd::info_kernel<double>, g, b, 0, s, dd::soa_of<double>(*st, first),
+                               distance ? (double*)distance + first : nullptr,
+                               speed ? (double*)speed + first : nullptr, len);
+    }
     return dd::finish();
 }
 

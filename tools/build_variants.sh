@@ -7,11 +7,22 @@ OUT=delivery_drone_amd/_native/lab
 mkdir -p $OUT
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I../include"
 build() { /opt/rocm/bin/hipcc $FLAGS "${@:2}" -o $OUT/lib_$1.so csrc/drone_step.hip & }
-build base
-build ocml -DDD_TRIG_OCML
-build strided -DDD_OBS_STRIDED
-build ntobs -DDD_NT_OBS
-build w8 -DDD_STEP_MIN_WAVES=8
-build w4 -DDD_STEP_MIN_WAVES=4
+# "prev": the committed source at $PREV_REV (default HEAD), for before/after runs
+if [ -n "${PREV_REV:-HEAD}" ] && git -C .. rev-parse -q --verify "${PREV_REV:-HEAD}" > /dev/null 2>&1; then
+  mkdir -p /tmp/dd_prev
+  git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/drone_step.hip" > /tmp/dd_prev/drone_step.hip
+  git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/trig.h" > /tmp/dd_prev/trig.h 2>/dev/null || true
+  /opt/rocm/bin/hipcc $FLAGS -Icsrc -o $OUT/lib_prev.so /tmp/dd_prev/drone_step.hip &
+fi
+for v in ${VARIANTS:-base}; do
+  case $v in
+    base) build base ;;
+    ocml) build ocml -DDD_TRIG_OCML ;;
+    plainobs) build plainobs -DDD_PLAIN_OBS_STORES ;;
+    w8) build w8 -DDD_STEP_MIN_WAVES=8 ;;
+    w4) build w4 -DDD_STEP_MIN_WAVES=4 ;;
+    *) echo "unknown variant $v" >&2; exit 1 ;;
+  esac
+done
 wait
 ls -la $OUT
