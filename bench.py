@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--cpu-baseline", type=float, default=10.0, help="seconds of CPU-baseline wall time (0 = skip)")
     p.add_argument("--cpu-workers", type=int, default=0, help="CPU-baseline processes (0 = min(16, cpus))")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--hbm-point", type=int, default=16_777_216,
+                   help="also time this many drones (HBM-resident) at N=1 and report it as hbm_point (0 = skip)")
     return p.parse_args()
 
 
@@ -97,6 +99,52 @@ def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
 
 
 # ------------------------------------------------------------------- GPU bench
+def time_steps(env, rows, steps, graph_steps, stream, write_obs=True):
+    """Replay `steps` frames from a hipGraph of `graph_steps` launches; returns
+    device ms per step (HIP events on the replay stream)."""
+    import torch
+    nrows = rows.shape[0]
+    with torch.cuda.stream(stream):
+        for k in range(3):
+            env.step(rows[k % nrows], write_obs=write_obs)
+        torch.cuda.synchronize(env.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for k in range(graph_steps):
+                env.step(rows[k % nrows], write_obs=write_obs)
+        g.replay()
+        torch.cuda.synchronize(env.device)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        reps = max(1, steps // graph_steps)
+        e0.record(stream)
+        for _ in range(reps):
+            g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize(env.device)
+    return e0.elapsed_time(e1) / (reps * graph_steps)
+
+
+def hbm_point(n, precision, seed, dev, write_obs):
+    """The same step at an HBM-resident batch (state + obs >> 256 MiB MALL):
+    the roofline the config-3 batch cannot show because it lives in cache."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg, precision=precision)
+    env.reset()
+    rows = torch.randint(0, 8, (4, n), device=dev, dtype=torch.uint8)
+    ms = time_steps(env, rows, 100, 10, torch.cuda.Stream(dev), write_obs)
+    bpe = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=write_obs)
+    gbs = bpe * n / (ms * 1e-3) / 1e9
+    out = {"envs": n, "us_per_step": round(ms * 1e3, 3), "steps_per_s": round(n / (ms * 1e-3), 1),
+           "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "traffic": pmc_traffic(n, precision, write_obs), "bytes_per_env": bpe}
+    del env, rows
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -188,6 +236,9 @@ def main():
 
     # sanity: the batch is alive and finite
     assert torch.isfinite(env.obs).all().item() and int(env.episode.max()) >= 1
+    hbm = None
+    if world == 1 and args.hbm_point > 0:
+        hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
 
     if rank == 0:
         total_steps = n * world * args.steps
@@ -234,6 +285,7 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            "hbm_point": hbm,
             "gpu_ms_per_step": round(step_ms, 6),
             "device": torch.cuda.get_device_name(dev),
         }

@@ -349,6 +349,18 @@ __device__ __forceinline__ E& at(E* base, uint32_t i) {
     return *reinterpret_cast<E*>(reinterpret_cast<B*>(base) + (uint32_t)(i * (uint32_t)sizeof(E)));
 }
 
+// Output streams this kernel never re-reads (reward, done) are stored
+// non-temporally, like the obs tile (+2-3 % at 262k and 16M lanes, lab3);
+// DD_PLAIN_OUT_STORES restores plain stores for A/B runs.
+template <typename E>
+__device__ __forceinline__ void put_out(E* base, uint32_t i, E v) {
+#ifdef DD_PLAIN_OUT_STORES
+    at(base, i) = v;
+#else
+    __builtin_nontemporal_store(v, &at(base, i));
+#endif
+}
+
 template <typename T>
 __device__ __forceinline__ void load_dynamics(const Soa<T>& a, uint32_t i, Lane& s) {
     s.x = at(a.x, i); s.y = at(a.y, i); s.vx = at(a.vx, i); s.vy = at(a.vy, i);
@@ -462,8 +474,8 @@ __global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArg
             at(a.steps, i) = s.steps;
             at(a.total, i) = (T)s.total;
         }
-        at(static_cast<T*>(p.reward), i) = (T)reward;
-        at(p.done, i) = (s.status & DD_ST_DONE) ? 1 : 0;
+        put_out(static_cast<T*>(p.reward), i, (T)reward);
+        put_out(p.done, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
         if (p.obs) observe(k, s, tile + threadIdx.x * DD_OBS_DIM);  // row -> LDS (stride 15: no bank conflict)
     }
     if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended

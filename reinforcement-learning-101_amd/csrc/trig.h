@@ -43,11 +43,21 @@ constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-
                  C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                  C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
 
+// Horner step a + z * b; fused unless DD_TRIG_NO_FMA (the polynomial tails
+// are far below an ulp of the result, so fusing only removes roundings).
+DD_HD inline double hstep(double a, double z, double b) {
+#ifdef DD_TRIG_NO_FMA
+    return a + z * b;
+#else
+    return fma(z, b, a);
+#endif
+}
+
 // sin(y0 + y1), |y0 + y1| <= pi/4, |y1| tiny
 DD_HD inline double ksin(double x, double y) {
     const double z = x * x;
     const double v = z * x;
-    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    const double r = hstep(S2, z, hstep(S3, z, hstep(S4, z, hstep(S5, z, S6))));
     return x - ((z * (0.5 * y - v * r) - y) - v * S1);
 }
 
@@ -55,7 +65,7 @@ DD_HD inline double ksin(double x, double y) {
 DD_HD inline double kcos(double x, double y) {
     const double z = x * x;
     const double w = z * z;
-    const double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    const double r = z * hstep(C1, z, hstep(C2, z, C3)) + w * w * hstep(C4, z, hstep(C5, z, C6));
     const double hz = 0.5 * z;
     const double u = 1.0 - hz;
     return u + (((1.0 - u) - hz) + (z * r - x * y));

@@ -19,6 +19,8 @@ for v in ${VARIANTS:-base}; do
     base) build base ;;
     ocml) build ocml -DDD_TRIG_OCML ;;
     plainobs) build plainobs -DDD_PLAIN_OBS_STORES ;;
+    nofma) build nofma -DDD_TRIG_NO_FMA ;;
+    plainout) build plainout -DDD_PLAIN_OUT_STORES ;;
     w8) build w8 -DDD_STEP_MIN_WAVES=8 ;;
     w4) build w4 -DDD_STEP_MIN_WAVES=4 ;;
     *) echo "unknown variant $v" >&2; exit 1 ;;

@@ -1,7 +1,8 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace,
-# N sweep, PMC traffic passes.  Every GPU step has its own time limit and the
-# steps are chained with && so the first failure ends the script.
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel traces
+# (config 3 and the 16M HBM point), PMC traffic passes.  Every GPU step has
+# its own time limit and the steps are chained with && so the first failure
+# ends the script.
 set -o pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
@@ -14,18 +15,10 @@ echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.s
 cat $OUT/smoke.log &&
 echo "== bench" && timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 cat $OUT/bench.json &&
-echo "== rocprofv3 kernel trace" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -f csv -- python3 bench.py --steps 2000 --warmup 200 --cpu-baseline 0 > $OUT/prof_bench.json 2> $OUT/prof.err &&
-echo "== sweep" && for N in 4096 65536 262144 1048576 4194304 16777216 67108864; do
-  S=$(( N >= 16777216 ? 200 : 2000 ));
-  timeout -k 10 300 python bench.py --envs-per-gpu $N --steps $S --warmup 20 --cpu-baseline 0 >> $OUT/sweep.jsonl 2>> $OUT/sweep.err || exit 1;
-done && cat $OUT/sweep.jsonl | python -c "
-import sys, json
-for l in sys.stdin:
-    d = json.loads(l); r = d['roofline']
-    print(d['config']['envs_per_gpu'], '%.3e steps/s' % d['value'], 'gpu_ms/step %.4f' % d['gpu_ms_per_step'], 'GB/s %.0f frac %.3f' % (r['achieved'], r['frac']))
-" &&
+echo "== rocprofv3 kernel trace (config 3)" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3 -o bench -f csv -- python3 bench.py --steps 2000 --warmup 200 --cpu-baseline 0 --hbm-point 0 > $OUT/prof_c3_bench.json 2> $OUT/prof.err &&
+echo "== rocprofv3 kernel trace (16M)" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_16m -o bench -f csv -- python3 bench.py --envs-per-gpu 16777216 --steps 200 --warmup 20 --cpu-baseline 0 --hbm-point 0 > $OUT/prof_16m_bench.json 2>> $OUT/prof.err &&
 echo "== pmc" && for N in 262144 16777216; do
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex step_kernel -d $OUT/pmc_${C}_$N -o pmc -f csv -- python3 bench.py --envs-per-gpu $N --steps 50 --warmup 5 --graph-steps 0 --cpu-baseline 0 > /dev/null 2>> $OUT/pmc.err || exit 1;
+    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex step_kernel -d $OUT/pmc_${C}_$N -o pmc -f csv -- python3 bench.py --envs-per-gpu $N --steps 50 --warmup 5 --graph-steps 0 --cpu-baseline 0 --hbm-point 0 > /dev/null 2>> $OUT/pmc.err || exit 1;
   done;
 done && echo "== done"
