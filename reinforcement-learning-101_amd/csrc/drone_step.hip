@@ -302,19 +302,25 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
 __device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o) {
     const DDConfig& c = k.c;
     const double dx = s.px - s.x, dy = s.py - s.y;
-    o[0] = (float)trig::div_exact(s.x, c.world_width, k.inv_w);
-    o[1] = (float)trig::div_exact(s.y, c.world_height, k.inv_h);
-    o[2] = (float)trig::div_exact(s.vx, c.vel_scale, k.inv_vel);
-    o[3] = (float)trig::div_exact(s.vy, c.vel_scale, k.inv_vel);
-    o[4] = (float)trig::div_exact(s.angle, c.angle_scale, k.inv_angle);
-    o[5] = (float)trig::div_exact(s.omega, c.vel_scale, k.inv_vel);
-    o[6] = (float)trig::div_exact(s.fuel, c.max_fuel, k.inv_fuel);
-    o[7] = (float)trig::div_exact(s.px, c.world_width, k.inv_w);
-    o[8] = (float)trig::div_exact(s.py, c.world_height, k.inv_h);
-    o[9] = (float)trig::div_exact(s.dist, c.world_width, k.inv_w);
-    o[10] = (float)trig::div_exact(dx, c.world_width, k.inv_w);
-    o[11] = (float)trig::div_exact(dy, c.world_height, k.inv_h);
-    o[12] = (float)trig::div_exact(s.speed, c.vel_scale, k.inv_vel);
+#ifdef DD_OBS_MUL  // experiment: x * RN(1/d), one op per column instead of three
+#define DD_Q(x, d, inv) ((x) * (inv))
+#else
+#define DD_Q(x, d, inv) trig::div_exact((x), (d), (inv))
+#endif
+    o[0] = (float)DD_Q(s.x, c.world_width, k.inv_w);
+    o[1] = (float)DD_Q(s.y, c.world_height, k.inv_h);
+    o[2] = (float)DD_Q(s.vx, c.vel_scale, k.inv_vel);
+    o[3] = (float)DD_Q(s.vy, c.vel_scale, k.inv_vel);
+    o[4] = (float)DD_Q(s.angle, c.angle_scale, k.inv_angle);
+    o[5] = (float)DD_Q(s.omega, c.vel_scale, k.inv_vel);
+    o[6] = (float)DD_Q(s.fuel, c.max_fuel, k.inv_fuel);
+    o[7] = (float)DD_Q(s.px, c.world_width, k.inv_w);
+    o[8] = (float)DD_Q(s.py, c.world_height, k.inv_h);
+    o[9] = (float)DD_Q(s.dist, c.world_width, k.inv_w);
+    o[10] = (float)DD_Q(dx, c.world_width, k.inv_w);
+    o[11] = (float)DD_Q(dy, c.world_height, k.inv_h);
+    o[12] = (float)DD_Q(s.speed, c.vel_scale, k.inv_vel);
+#undef DD_Q
     o[13] = (s.status & DD_ST_LANDED) ? 1.0f : 0.0f;
     o[14] = (s.status & DD_ST_CRASHED) ? 1.0f : 0.0f;
 }
@@ -438,63 +444,110 @@ struct StepArgs {
 #ifndef DD_STEP_MIN_WAVES
 #define DD_STEP_MIN_WAVES 1  // per SIMD; experiments raise it to force fewer VGPRs
 #endif
+#ifndef DD_LPT
+#define DD_LPT 1  // drones per thread (sub-tiles of 256 lanes per block)
+#endif
 
-template <typename T, int AFMT, bool kRef>
-__global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
-    __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
+// A lane's inputs as loaded (storage width), before widening to double.
+template <typename T>
+struct Raw {
+    T x, y, vx, vy, angle, omega, fuel, px, py, total;
+    uint32_t status, act;
+    int32_t steps;
+};
+
+template <typename T, int AFMT>
+__device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, uint32_t i, Raw<T>& r) {
+    r.x = at(a.x, i); r.y = at(a.y, i); r.vx = at(a.vx, i); r.vy = at(a.vy, i);
+    r.angle = at(a.angle, i); r.omega = at(a.omega, i); r.fuel = at(a.fuel, i);
+    r.px = at(a.px, i); r.py = at(a.py, i); r.total = at(a.total, i);
+    r.status = at(a.status, i);
+    r.steps = at(a.steps, i);
+    r.act = load_action<AFMT>(actions, i);
+}
+
+// Everything after the loads for one lane: the frame (or sticky done / auto
+// reset), the state and output stores, the observation row into `orow`
+// (LDS).  Returns whether the lane's episode ended in this call.
+template <typename T, bool kRef>
+__device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, uint32_t i, const Raw<T>& r,
+                                            float* orow) {
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
-    const uint32_t row0 = blockIdx.x * kBlock;
-    const uint32_t i = row0 + threadIdx.x;
-    const bool live = i < (uint32_t)p.n;
-    bool ended = false;  // episode ended in this call (for compaction)
-    if (live) {
-        Lane s;
-        load_dynamics(a, i, s);
-        s.status = at(a.status, i);
-        s.steps = at(a.steps, i);
-        s.total = at(a.total, i);
-        const uint32_t act = load_action<AFMT>(p.actions, i);
-        double reward;
-        if (s.status & DD_ST_DONE) {
-            reward = 0.0;
-            if (sw.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
-                s.episode = at(a.episode, i);
-                spawn(sw, a.env_id_base + i, s);
-                store_spawn(a, i, s);
-            } else {  // sticky done (game_engine.py:107-111): nothing changes
-                measure(s);
+    Lane s;
+    s.x = r.x; s.y = r.y; s.vx = r.vx; s.vy = r.vy; s.angle = r.angle; s.omega = r.omega;
+    s.fuel = r.fuel; s.px = r.px; s.py = r.py; s.total = r.total;
+    s.status = r.status;
+    s.steps = r.steps;
+    bool ended = false;
+    double reward;
+    if (s.status & DD_ST_DONE) {
+        reward = 0.0;
+        if (sw.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
+            s.episode = at(a.episode, i);
+            spawn(sw, a.env_id_base + i, s);
+            store_spawn(a, i, s);
+        } else {  // sticky done (game_engine.py:107-111): nothing changes
+            measure(s);
+        }
+    } else {
+#ifdef DD_EXP_NOMATH  // timing-only: same loads/stores, trivial arithmetic
+        s.x += s.vx; s.y += s.vy; s.angle += s.omega; s.fuel -= (double)r.act; s.steps += 1;
+        s.speed = s.vx; s.dist = s.vy;
+        reward = s.x;
+        s.status |= (s.y > 550.0) ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
+#else
+        reward = frame(k, sw, r.act, s);
+#endif
+        ended = (s.status & DD_ST_DONE) != 0;
+        store_dynamics(a, i, s);
+        if (sw.platform_moving) { at(a.px, i) = (T)s.px; at(a.status, i) = (uint8_t)s.status; }
+        else if (ended) at(a.status, i) = (uint8_t)s.status;
+        at(a.steps, i) = s.steps;
+        at(a.total, i) = (T)s.total;
+    }
+    put_out(static_cast<T*>(p.reward), i, (T)reward);
+    put_out(p.done, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+    if (p.obs) observe(k, s, orow);
+    return ended;
+}
+
+// dd_step kernel.  A block owns LPT consecutive 256-lane sub-tiles; each
+// thread loads its LPT lanes first, then finishes them one after the other,
+// so one sub-tile's stores and obs flush overlap the next one's arithmetic.
+template <typename T, int AFMT, bool kRef, int LPT>
+__global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
+    __shared__ __attribute__((aligned(16))) float tile[LPT][kBlock * DD_OBS_DIM];
+    const uint32_t base = blockIdx.x * (kBlock * LPT);
+    Raw<T> r[LPT];
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+        const uint32_t i = base + j * kBlock + threadIdx.x;
+        if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+        const uint32_t row0 = base + j * kBlock;
+        const uint32_t i = row0 + threadIdx.x;
+        const bool ended = i < (uint32_t)p.n && finish_lane<T, kRef>(p, a, i, r[j], tile[j] + threadIdx.x * DD_OBS_DIM);
+        if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
+            const uint64_t m = __ballot(ended);
+            if (m) {
+                const int lane = threadIdx.x & (kWave - 1);
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                int b = 0;
+                if (lane == leader) b = atomicAdd(p.done_count, __popcll(m));
+                b = __shfl(b, leader);
+                if (ended) p.done_idx[b + before] = p.idx_base + (int32_t)i;
             }
-        } else {
-            reward = frame(k, sw, act, s);
-            ended = (s.status & DD_ST_DONE) != 0;
-            store_dynamics(a, i, s);
-            if (sw.platform_moving) { at(a.px, i) = (T)s.px; at(a.status, i) = (uint8_t)s.status; }
-            else if (ended) at(a.status, i) = (uint8_t)s.status;
-            at(a.steps, i) = s.steps;
-            at(a.total, i) = (T)s.total;
         }
-        put_out(static_cast<T*>(p.reward), i, (T)reward);
-        put_out(p.done, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-        if (p.obs) observe(k, s, tile + threadIdx.x * DD_OBS_DIM);  // row -> LDS (stride 15: no bank conflict)
-    }
-    if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
-        const uint64_t m = __ballot(ended);
-        if (m) {
-            const int lane = threadIdx.x & (kWave - 1);
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            int base = 0;
-            if (lane == leader) base = atomicAdd(p.done_count, __popcll(m));
-            base = __shfl(base, leader);
-            if (ended) p.done_idx[base + before] = p.idx_base + (int32_t)i;
+        if (p.obs && row0 < (uint32_t)p.n) {  // uniform: the sub-tile leaves as 16-byte stores
+            __syncthreads();
+            const int rows = (int)min((uint32_t)kBlock, (uint32_t)p.n - row0);
+            flush_obs_tile(tile[j], p.obs + (size_t)row0 * DD_OBS_DIM, rows);
         }
-    }
-    if (p.obs) {  // uniform across the grid: the tile leaves as 16-byte stores
-        __syncthreads();
-        const int rows = (int)min((uint32_t)kBlock, (uint32_t)p.n - row0);
-        flush_obs_tile(tile, p.obs + (size_t)row0 * DD_OBS_DIM, rows);
     }
 }
 
@@ -623,7 +676,8 @@ bool state_ok(const DDState* st) {
 
 template <typename T, int AFMT, bool kRef>
 void launch_step(const StepArgs& p, const Soa<T>& a, hipStream_t s) {
-    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
+    const unsigned blocks = (unsigned)((p.n + kBlock * DD_LPT - 1) / (kBlock * DD_LPT));
+    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, DD_LPT>), dim3(blocks), dim3(kBlock), 0, s, p, a);
 }
 
 template <typename T, bool kRef>

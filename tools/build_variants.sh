@@ -21,6 +21,10 @@ for v in ${VARIANTS:-base}; do
     plainobs) build plainobs -DDD_PLAIN_OBS_STORES ;;
     nofma) build nofma -DDD_TRIG_NO_FMA ;;
     plainout) build plainout -DDD_PLAIN_OUT_STORES ;;
+    nomath) build nomath -DDD_EXP_NOMATH ;;
+    lpt2) build lpt2 -DDD_LPT=2 ;;
+    obsmul) build obsmul -DDD_OBS_MUL ;;
+    lpt4) build lpt4 -DDD_LPT=4 ;;
     w8) build w8 -DDD_STEP_MIN_WAVES=8 ;;
     w4) build w4 -DDD_STEP_MIN_WAVES=4 ;;
     *) echo "unknown variant $v" >&2; exit 1 ;;
