@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--cpu-baseline", type=float, default=10.0, help="seconds of CPU-baseline wall time (0 = skip)")
     p.add_argument("--cpu-workers", type=int, default=0, help="CPU-baseline processes (0 = min(16, cpus))")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                        "several ranks sharing one GPU)")
     p.add_argument("--hbm-point", type=int, default=16_777_216,
                    help="also time this many drones (HBM-resident) at N=1 and report it as hbm_point (0 = skip)")
     return p.parse_args()
@@ -165,10 +168,17 @@ def main():
 
     from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks but {ndev} visible GPUs: RCCL needs one GPU per rank")
+    local_dev = local % max(ndev, 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     n = args.envs_per_gpu
     cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=args.seed)
@@ -229,7 +239,8 @@ def main():
         wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
 
-    stats = torch.tensor([wall, gpu_ms], dtype=torch.float64, device=dev)
+    stats = torch.tensor([wall, gpu_ms], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     wall, gpu_ms = float(stats[0]), float(stats[1])
@@ -254,7 +265,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(n, args.precision, write_obs),
             "bytes_per_env": bytes_env,
-            "kernel": "dd::step_kernel<float,0>" if args.precision == "f32" else "dd::step_kernel<double,0>",
+            "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, 1>",
             "timing": "HIP events on the launch stream over the K timed steps / K",
         }
         out = {
