@@ -48,7 +48,10 @@ enum {
     DD_ACT_BITMASK = 0, /* uint8[N], bit0 = main, bit1 = left, bit2 = right  */
     DD_ACT_F32X3 = 1,   /* float[N][3] (main, left, right), nonzero = on;     */
                         /* the notebooks' Bernoulli(probs).sample() layout     */
-    DD_ACT_U8X3 = 2     /* uint8/bool[N][3] (main, left, right), nonzero = on */
+    DD_ACT_U8X3 = 2,    /* uint8/bool[N][3] (main, left, right), nonzero = on */
+    DD_ACT_PHILOX = 3   /* dd_rollout only: no action buffer; each frame's
+                           bitmask is Philox4x32-10(key = action_seed,
+                           ctr = {env, step}) & 7 — a uniform random policy */
 };
 
 /* Status byte bits (DDState.status). */
@@ -125,7 +128,7 @@ typedef struct DDConfig {
     uint64_t seed; /* Philox4x32-10 key for spawn draws */
 } DDConfig;
 
-/* The SoA.  Every pointer addresses N elements in device memory.  The eleven
+/* The SoA.  Every pointer addresses N elements in device memory.  The ten
  * floating-point arrays are float* (DD_F32) or double* (DD_F64). */
 typedef struct DDState {
     void *x, *y, *vx, *vy, *angle, *omega, *fuel; /* Drone: drone.py:19-33      */
@@ -153,12 +156,33 @@ typedef struct DDStepIO {
                              dd_step; required iff done_idx != NULL)             */
 } DDStepIO;
 
+/* Inputs and outputs of dd_rollout: `frames` consecutive frames, frame-major.
+ * Buffers are [frames][N] (actions in action_format, reward, done) and
+ * [frames][N][15] (obs).  The rollout equals `frames` dd_step calls with
+ * actions[k], bit for bit; the state stays in registers between frames. */
+typedef struct DDRolloutIO {
+    const void *actions;  /* [frames][N] per action_format; NULL for DD_ACT_PHILOX */
+    int32_t action_format;
+    int32_t frames;
+    void *reward;         /* float or double [frames][N] (required)             */
+    uint8_t *done;        /* uint8 [frames][N] (required)                       */
+    float *obs;           /* float [frames][N][15] (nullable)                   */
+    uint64_t action_seed; /* DD_ACT_PHILOX key                                  */
+    int64_t action_step;  /* DD_ACT_PHILOX counter of frame 0 (frame k: +k)     */
+} DDRolloutIO;
+
 /* Fills *cfg with config.py's values (randomize_platform = 1, others 0). */
 void dd_config_default(DDConfig *cfg);
 
 /* One frame for every lane: DroneGame.step (game_engine.py:95-138). */
 int dd_step(const DDConfig *cfg, const DDState *st, const DDStepIO *io,
             int64_t n, void *stream);
+
+/* `frames` consecutive frames in one launch (open-loop action sequences,
+ * random-policy collection, PPO-shaped rollouts with known actions): the
+ * same frame as dd_step, game_engine.py:95-138, applied frames times. */
+int dd_rollout(const DDConfig *cfg, const DDState *st, const DDRolloutIO *io,
+               int64_t n, void *stream);
 
 /* Re-spawn lanes (DroneGame.reset, game_engine.py:59-93).  mask: uint8 [N],
  * nonzero = reset that lane; NULL = all lanes.  obs (nullable) receives the

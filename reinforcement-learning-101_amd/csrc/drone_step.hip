@@ -551,6 +551,87 @@ __global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArg
     }
 }
 
+// ---------------------------------------------------------------------------
+// dd_rollout kernel: `frames` consecutive frames per launch, the lane's state
+// in registers between frames.  Per frame a lane reads its action (1 B, the
+// next frame's prefetched) and writes reward, done and its obs row (LDS tile,
+// double-buffered so one barrier per frame suffices).  Same frame code as
+// step_kernel, so a rollout equals `frames` dd_step calls bit for bit.
+// ---------------------------------------------------------------------------
+struct RolloutArgs {
+    Consts k;
+    const char* actions;      // frame 0, lane 0 of this chunk
+    int64_t act_stride;       // bytes between frames (N x action width)
+    char* reward;             // frame 0, lane 0 of this chunk
+    int64_t reward_stride;    // bytes between frames
+    uint8_t* done;
+    float* obs;               // frame 0, row 0 of this chunk (nullable)
+    int64_t n_total;          // N: frame stride in lanes for done / obs
+    int32_t frames;
+    int32_t n;                // lanes in this chunk
+    uint64_t action_seed;
+    int64_t action_step;
+};
+
+template <int AFMT>
+__device__ __forceinline__ uint32_t rollout_action(const RolloutArgs& p, int64_t env, int f, uint32_t i) {
+    if constexpr (AFMT == DD_ACT_PHILOX) {
+        const uint64_t step = (uint64_t)(p.action_step + f);
+        uint32_t r[4];
+        // ctr word 3 separates this stream from the spawn draws (which use 0)
+        philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)step,
+                      (uint32_t)(step >> 32) ^ 0xA5A5A5A5u, (uint32_t)p.action_seed,
+                      (uint32_t)(p.action_seed >> 32), r);
+        return r[0] & 7u;
+    } else {
+        return load_action<AFMT>(p.actions + f * p.act_stride, i);
+    }
+}
+
+template <typename T, int AFMT, bool kRef>
+__global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a) {
+    __shared__ __attribute__((aligned(16))) float tile[2][kBlock * DD_OBS_DIM];
+    const DDConfig& sw = p.k.c;
+    const Consts& k = kRef ? kRefConsts : p.k;
+    const uint32_t row0 = blockIdx.x * kBlock;
+    const uint32_t i = row0 + threadIdx.x;
+    const bool live = i < (uint32_t)p.n;
+    const int rows = (int)min((uint32_t)kBlock, (uint32_t)p.n - row0);
+    const int64_t env = a.env_id_base + i;
+    Lane s;
+    uint32_t next = 0;
+    if (live) {
+        load_dynamics(a, i, s);
+        s.total = at(a.total, i);
+        s.status = at(a.status, i);
+        s.steps = at(a.steps, i);
+        s.episode = at(a.episode, i);
+        next = rollout_action<AFMT>(p, env, 0, i);
+    }
+    for (int f = 0; f < p.frames; ++f) {
+        const uint32_t act = next;
+        float* orow = tile[f & 1] + threadIdx.x * DD_OBS_DIM;
+        if (live) {
+            if (f + 1 < p.frames) next = rollout_action<AFMT>(p, env, f + 1, i);
+            double reward = 0.0;
+            if (s.status & DD_ST_DONE) {
+                if (sw.auto_reset) spawn(sw, env, s);  // next-step reset
+                else measure(s);                       // sticky done
+            } else {
+                reward = frame(k, sw, act, s);
+            }
+            put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
+            put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+            if (p.obs) observe(k, s, orow);
+        }
+        if (p.obs) {  // uniform: all threads run every frame
+            __syncthreads();
+            flush_obs_tile(tile[f & 1], p.obs + ((size_t)f * p.n_total + row0) * DD_OBS_DIM, rows);
+        }
+    }
+    if (live) store_spawn(a, i, s);  // every field: lanes may have re-spawned
+}
+
 // dd_reset kernel: masked re-spawn (+ optional reset observation).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void reset_kernel(Consts k, Soa<T> a, const uint8_t* mask,
@@ -707,6 +788,42 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
     }
 }
 
+template <typename T, int AFMT, bool kRef>
+void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
+    hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
+}
+
+template <typename T, bool kRef>
+void launch_rollout_fmt(const RolloutArgs& p, int afmt, const Soa<T>& a, hipStream_t s) {
+    switch (afmt) {
+        case DD_ACT_BITMASK: launch_rollout<T, DD_ACT_BITMASK, kRef>(p, a, s); break;
+        case DD_ACT_F32X3: launch_rollout<T, DD_ACT_F32X3, kRef>(p, a, s); break;
+        case DD_ACT_U8X3: launch_rollout<T, DD_ACT_U8X3, kRef>(p, a, s); break;
+        default: launch_rollout<T, DD_ACT_PHILOX, kRef>(p, a, s); break;
+    }
+}
+
+template <typename T>
+void rollout_chunks(RolloutArgs p, const DDState& st, const DDRolloutIO& io, int64_t n, hipStream_t s) {
+    const bool ref = uses_reference_physics(p.k.c);
+    const int64_t act_w = io.action_format == DD_ACT_F32X3 ? 12 : io.action_format == DD_ACT_U8X3 ? 3
+                        : io.action_format == DD_ACT_BITMASK ? 1 : 0;
+    p.act_stride = n * act_w;
+    p.reward_stride = n * (int64_t)sizeof(T);
+    p.n_total = n;
+    for (int64_t first = 0; first < n; first += kChunk) {
+        const int64_t len = n - first < kChunk ? n - first : kChunk;
+        p.actions = io.actions ? static_cast<const char*>(io.actions) + first * act_w : nullptr;
+        p.reward = reinterpret_cast<char*>(static_cast<T*>(io.reward) + first);
+        p.done = io.done + first;
+        p.obs = io.obs ? io.obs + first * DD_OBS_DIM : nullptr;
+        p.n = (int32_t)len;
+        const Soa<T> a = soa_of<T>(st, first);
+        if (ref) launch_rollout_fmt<T, true>(p, io.action_format, a, s);
+        else launch_rollout_fmt<T, false>(p, io.action_format, a, s);
+    }
+}
+
 int finish() { return (int)hipGetLastError(); }
 
 }  // namespace dd
@@ -735,6 +852,24 @@ int dd_step(const DDConfig* cfg, const DDState* st, const DDStepIO* io, int64_t 
     p.done_count = io->done_count;
     if (st->precision == DD_F32) dd::step_chunks<float>(p, *st, *io, n, s);
     else dd::step_chunks<double>(p, *st, *io, n, s);
+    return dd::finish();
+}
+
+int dd_rollout(const DDConfig* cfg, const DDState* st, const DDRolloutIO* io, int64_t n, void* stream) {
+    if (!cfg || !io || !st || n < 0 || n > INT32_MAX || io->frames < 0) return hipErrorInvalidValue;
+    if (io->action_format < DD_ACT_BITMASK || io->action_format > DD_ACT_PHILOX) return hipErrorInvalidValue;
+    if (st->precision != DD_F32 && st->precision != DD_F64) return hipErrorInvalidValue;
+    if (n == 0 || io->frames == 0) return 0;
+    if (!dd::state_ok(st) || !io->reward || !io->done) return hipErrorInvalidValue;
+    if (io->action_format != DD_ACT_PHILOX && !io->actions) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    dd::RolloutArgs p{};
+    p.k = dd::make_consts(*cfg);
+    p.frames = io->frames;
+    p.action_seed = io->action_seed;
+    p.action_step = io->action_step;
+    if (st->precision == DD_F32) dd::rollout_chunks<float>(p, *st, *io, n, s);
+    else dd::rollout_chunks<double>(p, *st, *io, n, s);
     return dd::finish();
 }
 

@@ -13,14 +13,15 @@ import threading
 import torch  # noqa: F401  -- must be loaded first so the library binds torch's HIP runtime
 
 __all__ = [
-    "DD_F32", "DD_F64", "DD_ACT_BITMASK", "DD_ACT_F32X3", "DD_ACT_U8X3",
+    "DD_F32", "DD_F64", "DD_ACT_BITMASK", "DD_ACT_F32X3", "DD_ACT_U8X3", "DD_ACT_PHILOX",
     "DD_ST_DONE", "DD_ST_LANDED", "DD_ST_CRASHED", "DD_ST_PLAT_LEFT", "DD_OBS_DIM",
-    "DDConfig", "DDState", "DDStepIO", "lib", "library_path", "check", "NativeLibraryError",
+    "DDConfig", "DDState", "DDStepIO", "DDRolloutIO", "lib", "load", "library_path", "check",
+    "NativeLibraryError",
 ]
 
 DD_ABI_VERSION = 1
 DD_F32, DD_F64 = 0, 1
-DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3 = 0, 1, 2
+DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
 DD_OBS_DIM = 15
 
@@ -77,11 +78,21 @@ class DDStepIO(ctypes.Structure):
     ]
 
 
+class DDRolloutIO(ctypes.Structure):
+    _fields_ = [
+        ("actions", ctypes.c_void_p), ("action_format", _I), ("frames", _I),
+        ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+        ("action_seed", ctypes.c_uint64), ("action_step", ctypes.c_int64),
+    ]
+
+
 #: every symbol include/dronestep.h declares, with its ctypes signature
 EXPORTS = {
     "dd_config_default": (None, [ctypes.POINTER(DDConfig)]),
     "dd_step": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState),
                                ctypes.POINTER(DDStepIO), ctypes.c_int64, ctypes.c_void_p]),
+    "dd_rollout": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState),
+                                  ctypes.POINTER(DDRolloutIO), ctypes.c_int64, ctypes.c_void_p]),
     "dd_reset": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "dd_write_obs": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,

@@ -100,6 +100,20 @@ def test_argument_errors_return_invalid_value_without_gpu():
     assert lib.dd_write_obs(ctypes.byref(cfg), ctypes.byref(_state()), None, 4, None) == EINVAL
     assert lib.dd_reset(ctypes.byref(cfg), ctypes.byref(bad), None, None, 0, None) == 0  # empty batch
     assert lib.dd_compact(None, 0, None, None, None, 4, None) == EINVAL
+    rio = abi.DDRolloutIO()
+    rio.frames = 4
+    rio.action_format = 0  # bitmask needs an action buffer
+    rio.reward = rio.done = 8
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.action_format = 4
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.action_format, rio.frames = 3, -1
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.frames = 0  # nothing to do
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == 0
+    io.done_idx = None
+    io.action_format = 3  # Philox actions are rollout-only
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
     assert lib.dd_error_string(EINVAL)
 
 
