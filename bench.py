@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks sharing one GPU)")
+    p.add_argument("--rollout-point", type=int, default=65_536,
+                   help="also time BASELINE config 5 (this many envs x 256 frames via dd_rollout) at N=1 "
+                        "and report it as rollout_point (0 = skip)")
     p.add_argument("--hbm-point", type=int, default=16_777_216,
                    help="also time this many drones (HBM-resident) at N=1 and report it as hbm_point (0 = skip)")
     return p.parse_args()
@@ -144,6 +147,46 @@ def hbm_point(n, precision, seed, dev, write_obs):
            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
            "traffic": pmc_traffic(n, precision, write_obs), "bytes_per_env": bpe}
     del env, rows
+    torch.cuda.empty_cache()
+    return out
+
+
+def rollout_point(n, frames, precision, seed, dev):
+    """BASELINE config 5, the PPO rollout shape: n envs x `frames` frames,
+    reward + done fused into the step kernel, obs written into a
+    [frames, n, 15] rollout buffer — one dd_rollout launch per rollout, actions
+    read from a resident [frames, n] buffer.  Bytes per env-frame: action 1 +
+    reward 4 + done 1 + obs 60 (state in/out once per rollout)."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg, precision=precision)
+    env.reset()
+    acts = torch.randint(0, 8, (frames, n), device=dev, dtype=torch.uint8)
+    obs = torch.empty(frames, n, 15, device=dev)
+    rew = torch.empty(frames, n, device=dev, dtype=env.float_dtype)
+    done = torch.empty(frames, n, device=dev, dtype=torch.bool)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)  # warm-up
+        torch.cuda.synchronize(dev)
+        reps = 10
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    fbytes = 1 + rew.element_size() + 1 + 60
+    state = env.step_bytes_per_env(with_obs=False) - 1 - rew.element_size() - 1  # state read + write once
+    total = n * frames * fbytes + n * state
+    gbs = total / (ms * 1e-3) / 1e9
+    out = {"envs": n, "frames": frames, "ms_per_rollout": round(ms, 4),
+           "steps_per_s": round(n * frames / (ms * 1e-3), 1), "achieved": round(gbs, 1),
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env_frame": fbytes,
+           "kernel": "dd::rollout_kernel (dd_rollout, one launch per 256-frame rollout)"}
+    del env, acts, obs, rew, done
     torch.cuda.empty_cache()
     return out
 
@@ -250,6 +293,9 @@ def main():
     hbm = None
     if world == 1 and args.hbm_point > 0:
         hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
+    c5 = None
+    if world == 1 and args.rollout_point > 0:
+        c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
 
     if rank == 0:
         total_steps = n * world * args.steps
@@ -297,6 +343,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "hbm_point": hbm,
+            "rollout_point": c5,
             "gpu_ms_per_step": round(step_ms, 6),
             "device": torch.cuda.get_device_name(dev),
         }

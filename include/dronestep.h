@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 1
+#define DD_ABI_VERSION 2
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -154,6 +154,18 @@ typedef struct DDStepIO {
                              order (nullable; wave-ballot compaction)            */
     int32_t *done_count;  /* number of entries written to done_idx (zeroed by
                              dd_step; required iff done_idx != NULL)             */
+    /* The notebooks' shaped reward, fused (all three pointers set, or none):
+     * calc_reward(state, prev_state) of Actor_Critic_PPO.ipynb:164-263 on the
+     * frame's double-precision observation, with prev_state the state two
+     * frames back as collect_episodes_ppo passes it (:797-917), plus its
+     * max_steps truncation (:886-888: steps >= max_steps ends the episode,
+     * -500 unless landed; the lane's done bit is set so it stops / re-spawns). */
+    double *shaped_hist;  /* [2][N] per-lane distance history, slot = steps & 1;
+                             NaN = no previous state (dd_shaped_reset fills it) */
+    void *shaped_reward;  /* float or double [N] by precision                   */
+    uint8_t *shaped_done; /* uint8 [N]: done or truncated                        */
+    int32_t max_steps;    /* <= 0: no truncation                                 */
+    int32_t _pad2;
 } DDStepIO;
 
 /* Inputs and outputs of dd_rollout: `frames` consecutive frames, frame-major.
@@ -189,6 +201,12 @@ int dd_rollout(const DDConfig *cfg, const DDState *st, const DDRolloutIO *io,
  * reset observation of the reset lanes; other rows are left untouched. */
 int dd_reset(const DDConfig *cfg, const DDState *st, const uint8_t *mask,
              float *obs, int64_t n, void *stream);
+
+/* (Re)start the shaped-reward history of the masked lanes (NULL = all) from
+ * their current state: slot 0 = this state's distance, slot 1 = none.  Call
+ * after dd_reset; auto-reset inside dd_step restarts it by itself. */
+int dd_shaped_reset(const DDConfig *cfg, const DDState *st, const uint8_t *mask,
+                    double *shaped_hist, int64_t n, void *stream);
 
 /* Observation rows from the current state (DroneGame.get_state). */
 int dd_write_obs(const DDConfig *cfg, const DDState *st, float *obs,

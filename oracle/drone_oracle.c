@@ -212,6 +212,54 @@ void ora_observe(const DDConfig *c, const OraLane *s, double o[DD_OBS_DIM]) {
     o[14] = (s->status & DD_ST_CRASHED) ? 1.0 : 0.0;
 }
 
+/* ---- the notebooks' shaped reward ----------------------------------------*/
+/* calc_reward(state, prev_state)['total'], Actor_Critic_PPO.ipynb:164-263;
+ * o = get_state's doubles (state_to_array order), prev_dist NaN = None. */
+double ora_notebook_reward(const double o[DD_OBS_DIM], double prev_dist) {
+    double vx = o[2], vy = o[3], angle = o[4], fuel = o[6], dist = o[9], dx = o[10], dy = o[11], speed = o[12];
+    int landed = o[13] != 0.0, crashed = o[14] != 0.0;
+    double total = 0;
+    total += -0.5;
+    double distance = 0, hovering = 0;
+    if (!isnan(prev_dist)) {
+        double delta = prev_dist - dist;
+        double vtp = 0.0;
+        if (dist > 1e-6) vtp = (vx * dx + vy * dy) / dist;
+        if (speed >= 0.15 && vtp > 0.1 && dist > 0.065) {
+            double mult = 1.0 + speed * 2.0;
+            double v = delta * 1000 * mult;
+            distance = v < -2 ? -2 : (v > 5 ? 5 : v); /* np.clip */
+        } else if (delta < -0.001) {
+            distance = -2.0 * fabs(delta) * 1000;
+            hovering = 0;
+        } else if (speed < 0.05) {
+            hovering = -1.0;
+        } else if (speed < 0.15) {
+            hovering = -0.3;
+        } else {
+            distance = 0.0;
+        }
+    }
+    total += distance;
+    total += hovering;
+    double max_permissible = ((0.20 - 0.111) * dist) + 0.111;
+    double excess = fabs(angle) - max_permissible;
+    total += -(excess > 0 ? excess : 0);
+    if (dist < 1) total += -2 * ((speed - 0.1) > 0 ? speed - 0.1 : 0);
+    else total += -1 * ((speed - 0.6) > 0 ? speed - 0.6 : 0);
+    if (dy > 0) total += 0;
+    else total += dy * 4.0;
+    double terminal = 0;
+    if (landed) {
+        terminal = 800.0 + fuel * 100.0;
+    } else if (crashed) {
+        terminal = -200.0;
+        if (dist > 0.3) terminal -= 100.0;
+    }
+    total += terminal;
+    return total;
+}
+
 /* ---- SoA batch entry points (host arrays, DDState layout) ----------------*/
 #define FLD(name) (st->precision == DD_F64 ? ((double *)st->name)[i] : (double)((float *)st->name)[i])
 #define PUT(name, v)                                                \
@@ -249,25 +297,61 @@ static void emit_obs(const DDConfig *c, const OraLane *s, int64_t i, float *obs,
 }
 
 /* dd_step semantics over host arrays; actions are DD_ACT_BITMASK bytes.
- * reward is float or double by st->precision. */
-int ora_step(const DDConfig *c, const DDState *st, const uint8_t *actions, void *reward, uint8_t *done,
-             float *obs, double *obs64, int64_t n) {
+ * reward is float or double by st->precision.  hist/shaped/shaped_done
+ * (all or none) add the notebooks' reward: hist is [2][n] doubles, slot
+ * steps & 1 holds the distance of the state two frames back (NaN = None),
+ * max_steps > 0 adds collect_episodes_ppo's timeout. */
+int ora_step_shaped(const DDConfig *c, const DDState *st, const uint8_t *actions, void *reward, uint8_t *done,
+                    float *obs, double *obs64, double *hist, void *shaped, uint8_t *shaped_done,
+                    int32_t max_steps, int64_t n) {
     for (int64_t i = 0; i < n; ++i) {
         OraLane s;
         load_lane(st, i, &s);
-        double r = 0.0;
+        double r = 0.0, sr = 0.0;
+        int sd = 0;
         if (s.status & DD_ST_DONE) {
-            if (c->auto_reset) ora_spawn(c, st->env_id_base + i, &s);
+            if (c->auto_reset) {
+                ora_spawn(c, st->env_id_base + i, &s);
+                if (hist) {
+                    hist[i] = dist2d(s.x, s.y, s.px, s.py) / c->world_width;
+                    hist[n + i] = NAN;
+                }
+            } else {
+                sd = 1;
+            }
         } else {
             r = ora_frame(c, actions[i], &s);
+            if (hist) {
+                double o[DD_OBS_DIM];
+                ora_observe(c, &s, o);
+                double *slot = hist + (s.steps & 1) * n;
+                sr = ora_notebook_reward(o, slot[i]);
+                slot[i] = o[9];
+                sd = (s.status & DD_ST_DONE) != 0;
+                if (max_steps > 0 && s.steps >= max_steps) {
+                    if (!(s.status & DD_ST_LANDED)) sr -= 500;
+                    sd = 1;
+                    s.status |= DD_ST_DONE;
+                }
+            }
         }
         store_lane(st, i, &s);
         if (st->precision == DD_F64) ((double *)reward)[i] = r;
         else ((float *)reward)[i] = (float)r;
         done[i] = (s.status & DD_ST_DONE) ? 1 : 0;
+        if (hist) {
+            if (st->precision == DD_F64) ((double *)shaped)[i] = sr;
+            else ((float *)shaped)[i] = (float)sr;
+            shaped_done[i] = (uint8_t)sd;
+        }
         emit_obs(c, &s, i, obs, obs64);
     }
     return 0;
+}
+
+int ora_step(const DDConfig *c, const DDState *st, const uint8_t *actions, void *reward, uint8_t *done,
+             float *obs, double *obs64, int64_t n) {
+    return ora_step_shaped(c, st, actions, reward, done, obs, obs64, NULL, NULL, NULL, 0, n);
 }
 
 int ora_reset(const DDConfig *c, const DDState *st, const uint8_t *mask, float *obs, double *obs64, int64_t n) {

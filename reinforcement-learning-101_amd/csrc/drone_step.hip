@@ -297,9 +297,10 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     return reward;
 }
 
-// DroneGame.get_state (game_engine.py:140-177) in state_to_array order;
+// DroneGame.get_state (game_engine.py:140-177) in state_to_array order, as the
+// reference's doubles (columns 0-12; 13/14 are the landed / crashed flags);
 // measure() has run on `s`.
-__device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o) {
+__device__ __forceinline__ void observe_values(const Consts& k, const Lane& s, double v[13]) {
     const DDConfig& c = k.c;
     const double dx = s.px - s.x, dy = s.py - s.y;
 #ifdef DD_OBS_MUL  // experiment: x * RN(1/d), one op per column instead of three
@@ -307,22 +308,65 @@ __device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o
 #else
 #define DD_Q(x, d, inv) trig::div_exact((x), (d), (inv))
 #endif
-    o[0] = (float)DD_Q(s.x, c.world_width, k.inv_w);
-    o[1] = (float)DD_Q(s.y, c.world_height, k.inv_h);
-    o[2] = (float)DD_Q(s.vx, c.vel_scale, k.inv_vel);
-    o[3] = (float)DD_Q(s.vy, c.vel_scale, k.inv_vel);
-    o[4] = (float)DD_Q(s.angle, c.angle_scale, k.inv_angle);
-    o[5] = (float)DD_Q(s.omega, c.vel_scale, k.inv_vel);
-    o[6] = (float)DD_Q(s.fuel, c.max_fuel, k.inv_fuel);
-    o[7] = (float)DD_Q(s.px, c.world_width, k.inv_w);
-    o[8] = (float)DD_Q(s.py, c.world_height, k.inv_h);
-    o[9] = (float)DD_Q(s.dist, c.world_width, k.inv_w);
-    o[10] = (float)DD_Q(dx, c.world_width, k.inv_w);
-    o[11] = (float)DD_Q(dy, c.world_height, k.inv_h);
-    o[12] = (float)DD_Q(s.speed, c.vel_scale, k.inv_vel);
+    v[0] = DD_Q(s.x, c.world_width, k.inv_w);
+    v[1] = DD_Q(s.y, c.world_height, k.inv_h);
+    v[2] = DD_Q(s.vx, c.vel_scale, k.inv_vel);
+    v[3] = DD_Q(s.vy, c.vel_scale, k.inv_vel);
+    v[4] = DD_Q(s.angle, c.angle_scale, k.inv_angle);
+    v[5] = DD_Q(s.omega, c.vel_scale, k.inv_vel);
+    v[6] = DD_Q(s.fuel, c.max_fuel, k.inv_fuel);
+    v[7] = DD_Q(s.px, c.world_width, k.inv_w);
+    v[8] = DD_Q(s.py, c.world_height, k.inv_h);
+    v[9] = DD_Q(s.dist, c.world_width, k.inv_w);
+    v[10] = DD_Q(dx, c.world_width, k.inv_w);
+    v[11] = DD_Q(dy, c.world_height, k.inv_h);
+    v[12] = DD_Q(s.speed, c.vel_scale, k.inv_vel);
 #undef DD_Q
-    o[13] = (s.status & DD_ST_LANDED) ? 1.0f : 0.0f;
-    o[14] = (s.status & DD_ST_CRASHED) ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ void write_obs_row(const double v[13], uint32_t status, float* o) {
+#pragma unroll
+    for (int j = 0; j < 13; ++j) o[j] = (float)v[j];
+    o[13] = (status & DD_ST_LANDED) ? 1.0f : 0.0f;
+    o[14] = (status & DD_ST_CRASHED) ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o) {
+    double v[13];
+    observe_values(k, s, v);
+    write_obs_row(v, s.status, o);
+}
+
+// calc_reward(state, prev_state)['total'] of Actor_Critic_PPO.ipynb:164-263
+// (scalers: rl_helpers/scalers.py) on the frame's double observation `v`;
+// prev_dist is prev_state.distance_to_platform, NaN for prev_state None.  The
+// terms are summed in the notebook's order.  Branch-free (see frame()).
+__device__ __forceinline__ double notebook_reward(const double v[13], uint32_t status, double prev_dist) {
+    const double vx = v[2], vy = v[3], angle = v[4], fuel = v[6], dist = v[9], dx = v[10], dy = v[11],
+                 speed = v[12];
+    const bool have_prev = !__builtin_isnan(prev_dist);
+    const double delta = prev_dist - dist;
+    const double vtp = dist > 1e-6 ? (vx * dx + vy * dy) / dist : 0.0;  // velocity toward platform
+    const bool fast_toward = (speed >= 0.15) & (vtp > 0.1) & (dist > 0.065);
+    const double clipped = fmin(fmax(delta * 1000 * (1.0 + speed * 2.0), -2.0), 5.0);  // np.clip
+    const bool away = !fast_toward & (delta < -0.001);
+    double distance = fast_toward ? clipped : away ? -2.0 * fabs(delta) * 1000 : 0.0;
+    double hovering = (fast_toward | away) ? 0.0 : speed < 0.05 ? -1.0 : speed < 0.15 ? -0.3 : 0.0;
+    distance = have_prev ? distance : 0.0;
+    hovering = have_prev ? hovering : 0.0;
+    double total = 0.0;
+    total += -0.5;
+    total += distance;
+    total += hovering;
+    const double excess = fabs(angle) - (((0.20 - 0.111) * dist) + 0.111);
+    total += -(excess > 0.0 ? excess : 0.0);
+    const double over = dist < 1 ? speed - 0.1 : speed - 0.6;
+    total += (dist < 1 ? -2.0 : -1.0) * (over > 0.0 ? over : 0.0);
+    total += dy > 0.0 ? 0.0 : dy * 4.0;
+    const bool landed = status & DD_ST_LANDED, crashed = status & DD_ST_CRASHED;
+    const double crash_term = dist > 0.3 ? -200.0 - 100.0 : -200.0;
+    total += landed ? 800.0 + fuel * 100.0 : crashed ? crash_term : 0.0;
+    return total;
 }
 
 // ---------------------------------------------------------------------------
@@ -439,6 +483,11 @@ struct StepArgs {
     int32_t* done_count;
     int32_t n;             // lanes in this chunk
     int32_t idx_base;      // chunk start, for done_idx entries
+    double* shaped_hist;   // slot 0 of this chunk; slot 1 at + hist_stride
+    int64_t hist_stride;
+    void* shaped_reward;
+    uint8_t* shaped_done;
+    int32_t max_steps;
 };
 
 #ifndef DD_STEP_MIN_WAVES
@@ -469,7 +518,7 @@ __device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, u
 // Everything after the loads for one lane: the frame (or sticky done / auto
 // reset), the state and output stores, the observation row into `orow`
 // (LDS).  Returns whether the lane's episode ended in this call.
-template <typename T, bool kRef>
+template <typename T, bool kRef, bool kShaped>
 __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, uint32_t i, const Raw<T>& r,
                                             float* orow) {
     const DDConfig& sw = p.k.c;
@@ -481,14 +530,21 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     s.steps = r.steps;
     bool ended = false;
     double reward;
+    double shaped = 0.0;
+    bool shaped_done = false;
     if (s.status & DD_ST_DONE) {
         reward = 0.0;
         if (sw.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
             s.episode = at(a.episode, i);
             spawn(sw, a.env_id_base + i, s);
             store_spawn(a, i, s);
+            if constexpr (kShaped) {  // the notebook's history restarts: prev_state None
+                at(p.shaped_hist, i) = trig::div_exact(s.dist, k.c.world_width, k.inv_w);
+                at(p.shaped_hist + p.hist_stride, i) = __builtin_nan("");
+            }
         } else {  // sticky done (game_engine.py:107-111): nothing changes
             measure(s);
+            shaped_done = true;
         }
     } else {
 #ifdef DD_EXP_NOMATH  // timing-only: same loads/stores, trivial arithmetic
@@ -499,6 +555,20 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
 #else
         reward = frame(k, sw, r.act, s);
 #endif
+        if constexpr (kShaped) {
+            double v[13];
+            observe_values(k, s, v);
+            double* slot = p.shaped_hist + (s.steps & 1) * p.hist_stride;  // two frames back
+            shaped = notebook_reward(v, s.status, at(slot, i));
+            at(slot, i) = v[9];
+            shaped_done = (s.status & DD_ST_DONE) != 0;
+            if (p.max_steps > 0 && s.steps >= p.max_steps) {  // collect_episodes_ppo timeout
+                shaped = (s.status & DD_ST_LANDED) ? shaped : shaped - 500;
+                shaped_done = true;
+                s.status |= DD_ST_DONE;  // the episode ends here (TimeLimit)
+            }
+            if (p.obs) write_obs_row(v, s.status, orow);
+        }
         ended = (s.status & DD_ST_DONE) != 0;
         store_dynamics(a, i, s);
         if (sw.platform_moving) { at(a.px, i) = (T)s.px; at(a.status, i) = (uint8_t)s.status; }
@@ -508,14 +578,20 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     }
     put_out(static_cast<T*>(p.reward), i, (T)reward);
     put_out(p.done, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-    if (p.obs) observe(k, s, orow);
+    if constexpr (kShaped) {
+        put_out(static_cast<T*>(p.shaped_reward), i, (T)shaped);
+        put_out(p.shaped_done, i, (uint8_t)(shaped_done ? 1 : 0));
+        if (p.obs && ((r.status & DD_ST_DONE) != 0)) observe(k, s, orow);  // the live path wrote its row
+    } else {
+        if (p.obs) observe(k, s, orow);
+    }
     return ended;
 }
 
 // dd_step kernel.  A block owns LPT consecutive 256-lane sub-tiles; each
 // thread loads its LPT lanes first, then finishes them one after the other,
 // so one sub-tile's stores and obs flush overlap the next one's arithmetic.
-template <typename T, int AFMT, bool kRef, int LPT>
+template <typename T, int AFMT, bool kRef, bool kShaped, int LPT>
 __global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
     __shared__ __attribute__((aligned(16))) float tile[LPT][kBlock * DD_OBS_DIM];
     const uint32_t base = blockIdx.x * (kBlock * LPT);
@@ -529,7 +605,8 @@ __global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArg
     for (int j = 0; j < LPT; ++j) {
         const uint32_t row0 = base + j * kBlock;
         const uint32_t i = row0 + threadIdx.x;
-        const bool ended = i < (uint32_t)p.n && finish_lane<T, kRef>(p, a, i, r[j], tile[j] + threadIdx.x * DD_OBS_DIM);
+        const bool ended =
+            i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r[j], tile[j] + threadIdx.x * DD_OBS_DIM);
         if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
             const uint64_t m = __ballot(ended);
             if (m) {
@@ -588,6 +665,14 @@ __device__ __forceinline__ uint32_t rollout_action(const RolloutArgs& p, int64_t
     }
 }
 
+// The state between two frames is what dd_step would store: rounded to the
+// storage width T (a no-op for double).
+template <typename T>
+__device__ __forceinline__ void quantize(Lane& s) {
+    s.x = (T)s.x; s.y = (T)s.y; s.vx = (T)s.vx; s.vy = (T)s.vy; s.angle = (T)s.angle;
+    s.omega = (T)s.omega; s.fuel = (T)s.fuel; s.px = (T)s.px; s.py = (T)s.py; s.total = (T)s.total;
+}
+
 template <typename T, int AFMT, bool kRef>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a) {
     __shared__ __attribute__((aligned(16))) float tile[2][kBlock * DD_OBS_DIM];
@@ -623,6 +708,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
             put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
             put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
             if (p.obs) observe(k, s, orow);
+            quantize<T>(s);  // the obs above sees the unrounded frame, like dd_step's
         }
         if (p.obs) {  // uniform: all threads run every frame
             __syncthreads();
@@ -630,6 +716,21 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
         }
     }
     if (live) store_spawn(a, i, s);  // every field: lanes may have re-spawned
+}
+
+// dd_shaped_reset kernel: the notebook reward's history restarts from the
+// current state (slot 0 = its distance, slot 1 = none).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void shaped_reset_kernel(Consts k, Soa<T> a, const uint8_t* mask,
+                                                              double* hist, int64_t stride, int32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (uint32_t)n) return;
+    if (mask && !at(mask, i)) return;
+    Lane s;
+    load_dynamics(a, i, s);
+    measure(s);
+    at(hist, i) = trig::div_exact(s.dist, k.c.world_width, k.inv_w);
+    at(hist + stride, i) = __builtin_nan("");
 }
 
 // dd_reset kernel: masked re-spawn (+ optional reset observation).
@@ -755,18 +856,18 @@ bool state_ok(const DDState* st) {
            (st->precision == DD_F32 || st->precision == DD_F64);
 }
 
-template <typename T, int AFMT, bool kRef>
+template <typename T, int AFMT, bool kRef, bool kShaped>
 void launch_step(const StepArgs& p, const Soa<T>& a, hipStream_t s) {
     const unsigned blocks = (unsigned)((p.n + kBlock * DD_LPT - 1) / (kBlock * DD_LPT));
-    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, DD_LPT>), dim3(blocks), dim3(kBlock), 0, s, p, a);
+    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShaped, DD_LPT>), dim3(blocks), dim3(kBlock), 0, s, p, a);
 }
 
-template <typename T, bool kRef>
+template <typename T, bool kRef, bool kShaped>
 void launch_step_fmt(const StepArgs& p, int afmt, const Soa<T>& a, hipStream_t s) {
     switch (afmt) {
-        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK, kRef>(p, a, s); break;
-        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3, kRef>(p, a, s); break;
-        default: launch_step<T, DD_ACT_U8X3, kRef>(p, a, s); break;
+        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK, kRef, kShaped>(p, a, s); break;
+        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3, kRef, kShaped>(p, a, s); break;
+        default: launch_step<T, DD_ACT_U8X3, kRef, kShaped>(p, a, s); break;
     }
 }
 
@@ -782,9 +883,20 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
         p.obs = io.obs ? io.obs + first * DD_OBS_DIM : nullptr;
         p.n = (int32_t)len;
         p.idx_base = (int32_t)first;
+        const bool shaped = io.shaped_hist != nullptr;
+        p.shaped_hist = shaped ? io.shaped_hist + first : nullptr;
+        p.hist_stride = n;
+        p.shaped_reward = shaped ? static_cast<void*>(static_cast<T*>(io.shaped_reward) + first) : nullptr;
+        p.shaped_done = shaped ? io.shaped_done + first : nullptr;
+        p.max_steps = io.max_steps;
         const Soa<T> a = soa_of<T>(st, first);
-        if (ref) launch_step_fmt<T, true>(p, io.action_format, a, s);
-        else launch_step_fmt<T, false>(p, io.action_format, a, s);
+        if (ref) {
+            if (shaped) launch_step_fmt<T, true, true>(p, io.action_format, a, s);
+            else launch_step_fmt<T, true, false>(p, io.action_format, a, s);
+        } else {
+            if (shaped) launch_step_fmt<T, false, true>(p, io.action_format, a, s);
+            else launch_step_fmt<T, false, false>(p, io.action_format, a, s);
+        }
     }
 }
 
@@ -839,6 +951,8 @@ int dd_step(const DDConfig* cfg, const DDState* st, const DDStepIO* io, int64_t 
     if (io->action_format < DD_ACT_BITMASK || io->action_format > DD_ACT_U8X3) return hipErrorInvalidValue;
     if (st->precision != DD_F32 && st->precision != DD_F64) return hipErrorInvalidValue;
     if (io->done_idx && !io->done_count) return hipErrorInvalidValue;
+    const int shaped_ptrs = (io->shaped_hist != nullptr) + (io->shaped_reward != nullptr) + (io->shaped_done != nullptr);
+    if (shaped_ptrs != 0 && shaped_ptrs != 3) return hipErrorInvalidValue;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (io->done_count) {
         const hipError_t e = hipMemsetAsync(io->done_count, 0, sizeof(int32_t), s);
@@ -888,6 +1002,27 @@ int dd_reset(const DDConfig* cfg, const DDState* st, const uint8_t* mask, float*
             hipLaunchKernelGGL(dd::reset_kernel<float>, g, b, 0, s, k, dd::soa_of<float>(*st, first), m, o, len);
         else
             hipLaunchKernelGGL(dd::reset_kernel<double>, g, b, 0, s, k, dd::soa_of<double>(*st, first), m, o, len);
+    }
+    return dd::finish();
+}
+
+int dd_shaped_reset(const DDConfig* cfg, const DDState* st, const uint8_t* mask, double* hist, int64_t n,
+                    void* stream) {
+    if (!cfg || !st || n < 0 || n > INT32_MAX) return hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (!hist || !dd::state_ok(st)) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dd::Consts k = dd::make_consts(*cfg);
+    for (int64_t first = 0; first < n; first += dd::kChunk) {
+        const int32_t len = (int32_t)(n - first < dd::kChunk ? n - first : dd::kChunk);
+        const dim3 g((unsigned)dd::tiles_of(len)), b(dd::kBlock);
+        const uint8_t* m = mask ? mask + first : nullptr;
+        if (st->precision == DD_F32)
+            hipLaunchKernelGGL(dd::shaped_reset_kernel<float>, g, b, 0, s, k, dd::soa_of<float>(*st, first), m,
+                               hist + first, n, len);
+        else
+            hipLaunchKernelGGL(dd::shaped_reset_kernel<double>, g, b, 0, s, k, dd::soa_of<double>(*st, first), m,
+                               hist + first, n, len);
     }
     return dd::finish();
 }

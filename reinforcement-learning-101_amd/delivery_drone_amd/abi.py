@@ -19,7 +19,7 @@ __all__ = [
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 1
+DD_ABI_VERSION = 2
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
@@ -75,6 +75,8 @@ class DDStepIO(ctypes.Structure):
         ("actions", ctypes.c_void_p), ("action_format", _I), ("_pad", _I),
         ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("obs", ctypes.c_void_p),
         ("done_idx", ctypes.c_void_p), ("done_count", ctypes.c_void_p),
+        ("shaped_hist", ctypes.c_void_p), ("shaped_reward", ctypes.c_void_p), ("shaped_done", ctypes.c_void_p),
+        ("max_steps", _I), ("_pad2", _I),
     ]
 
 
@@ -95,6 +97,8 @@ EXPORTS = {
                                   ctypes.POINTER(DDRolloutIO), ctypes.c_int64, ctypes.c_void_p]),
     "dd_reset": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "dd_shaped_reset": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "dd_write_obs": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
                                     ctypes.c_int64, ctypes.c_void_p]),
     "dd_get_info": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,

@@ -347,9 +347,84 @@ def notebook_kats() -> dict:
            "dy_to_platform": -0.065495, "speed": 0.029699999999999997, "steps": 1}
     for k, v in nb2.items():
         assert st[k] == v, (k, st[k], v)
+    # the same cell prints calc_reward(state) with prev_state None (:309-316)
+    shaped = notebook_reward_fn()(st, None)
+    nb3 = {"time_penalty": -0.5717729518600626, "vertical_position": -0.26198, "total": -0.76198}
+    for k, v in nb3.items():
+        assert shaped[k] == v, (k, shaped[k], v)
     out["actor_critic_ppo"] = dict(source="Actor_Critic_PPO.ipynb:286-301",
-                                   start=dict(x=688, y=152, px=631, py=113), action=0, frames=1, expect=nb2)
+                                   start=dict(x=688, y=152, px=631, py=113), action=0, frames=1, expect=nb2,
+                                   shaped_source="Actor_Critic_PPO.ipynb:309-316", shaped_total=nb3["total"])
     return out
+
+
+# --------------------------------------------------------------------------
+# The notebooks' shaped reward
+# --------------------------------------------------------------------------
+def notebook_reward_fn():
+    """calc_reward from Actor_Critic_PPO.ipynb, executed from the notebook's
+    own cell source (read at generation time; nothing is copied)."""
+    import json as _json
+    import math
+    from types import SimpleNamespace
+    from delivery_drone.game.socket_client import DroneState
+    import rl_helpers.scalers as scalers
+    nb = _json.load(open(os.path.join(REF, "Actor_Critic_PPO.ipynb")))
+    ns = {"np": np, "math": math, "DroneState": DroneState}
+    ns.update({k: getattr(scalers, k) for k in dir(scalers) if not k.startswith("_")})
+    for cell in nb["cells"]:
+        src = "".join(cell["source"])
+        if cell["cell_type"] == "code" and ("def calc_velocity_alignment" in src or "def calc_reward" in src):
+            exec(compile(src, "Actor_Critic_PPO.ipynb", "exec"), ns)
+    calc = ns["calc_reward"]
+
+    def total(state_dict, prev_dist):
+        prev = None if prev_dist is None else SimpleNamespace(distance_to_platform=prev_dist)
+        return calc(SimpleNamespace(**state_dict), prev_state=prev)
+
+    return total
+
+
+def shaped_set(rng, counts: dict, max_steps: int = 300) -> dict:
+    """Single steps whose next_state goes through the notebook reward, with
+    prev_state None / near / far and step counts around max_steps; the
+    timeout rule of collect_episodes_ppo (Actor_Critic_PPO.ipynb:886-888)."""
+    reward = notebook_reward_fn()
+    ins = {}
+    for kind, m in counts.items():
+        for k, v in draw_states(rng, m, kind).items():
+            ins.setdefault(k, []).append(v)
+    ins = {k: np.concatenate(v) for k, v in ins.items()}
+    n = ins["x"].shape[0]
+    ins["done"][:] = False
+    ins["steps"] = np.where(rng.random(n) < 0.3, rng.integers(max_steps - 3, max_steps + 2, n),
+                            rng.integers(0, max_steps - 3, n)).astype(np.int32)
+    g = new_game()
+    prev = np.full(n, np.nan)
+    out_total, out_shaped, out_done, parts = [], [], [], []
+    for i in range(n):
+        s = {k: (v[i].item() if hasattr(v[i], "item") else v[i]) for k, v in ins.items()}
+        poke(g, s)
+        st, _, done, _ = g.step(act_dict(int(ins["action"][i])))
+        d = st["distance_to_platform"]
+        mode = rng.integers(0, 4)
+        pd = None if mode == 0 else d + rng.uniform(-0.004, 0.004) if mode == 1 else \
+            d + rng.choice([-0.001, 0.001, 0.0]) if mode == 2 else float(rng.uniform(0, 1.2))
+        prev[i] = np.nan if pd is None else pd
+        r = reward(st, pd)
+        tot = r["total"]
+        shaped, sdone = tot, bool(done)
+        if g.steps >= max_steps:
+            if not st["landed"]:
+                shaped -= 500
+            sdone = True
+        out_total.append(tot)
+        out_shaped.append(shaped)
+        out_done.append(sdone)
+    rec = {f"in_{k}": np.asarray(v) for k, v in ins.items()}
+    rec.update(in_prev=prev, max_steps=np.int32(max_steps), out_total=np.asarray(out_total),
+               out_shaped=np.asarray(out_shaped), out_shaped_done=np.asarray(out_done))
+    return rec
 
 
 def main():
@@ -377,6 +452,9 @@ def main():
                         **traj_batch(games=8, frames=300, seed=99, moving=True))
     with open(os.path.join(HERE, "reset_facts.json"), "w") as f:
         json.dump(reset_facts(), f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "shaped_reward.npz"),
+                        **shaped_set(np.random.default_rng(777), {"broad": 1200, "pad": 1200, "ground": 400,
+                                                                 "bounds": 200}))
     print("fixtures written to", HERE)
 
 

@@ -426,3 +426,64 @@ def test_large_batch_properties(gpu_device):
     np.testing.assert_array_equal(host(done)[lo:], odone)
     assert gd.f32_close(host(obs)[lo:], oobs, 1.0).all()
     assert gd.f32_close(host(reward)[lo:], oreward, 1.0).all()
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_notebook_reward_vs_reference(precision, gpu_device):
+    """the notebooks' calc_reward + max_steps timeout,
+    fused into the step, against the notebook's own outputs."""
+    rec = gd.npz("shaped_reward.npz")
+    n = rec["in_x"].shape[0]
+    env = VecDroneEnv(n, precision=precision, device=gpu_device, reward_mode="notebook",
+                      max_steps=int(rec["max_steps"]))
+    load(env, gd.state_from_inputs(rec))
+    hist = np.full((2, n), np.nan)
+    slot = (rec["in_steps"].astype(np.int64) + 1) & 1
+    hist[slot, np.arange(n)] = rec["in_prev"]
+    env.shaped_hist.copy_(torch.as_tensor(hist))
+    obs, shaped, sdone, info = env.step(torch.as_tensor(rec["in_action"], device=gpu_device))
+    np.testing.assert_array_equal(host(sdone), rec["out_shaped_done"])
+    want = rec["out_shaped"]
+    got = host(shaped).astype(np.float64)
+    if precision == "f64":
+        ok = f64_close(got, want, 8, 1e-9)  # |terms| up to ~2e3: 1e-9 covers 1-ulp trig in the inputs
+    else:
+        ok = gd.f32_close(got, want, 2.0, 1e-6)
+    assert ok.all(), np.flatnonzero(~ok)[:5]
+    # the engine's own reward is still there, unchanged
+    e_env, _, e_reward, e_done, _ = step_fixture(rec, precision, gpu_device)
+    assert np.array_equal(host(info["engine_reward"]), e_reward)
+
+
+def test_notebook_reward_kat_and_history(gpu_device):
+    k = gd.js("kat_notebooks.json")["actor_critic_ppo"]
+    env = VecDroneEnv(1, precision="f64", device=gpu_device, reward_mode="notebook")
+    env.reset()
+    load(env, gd.edge_case_state({"state": gd.base_state(**k["start"])}))
+    env.shaped_hist.fill_(float("nan"))
+    _, shaped, _, _ = env.step(torch.tensor([k["action"]], dtype=torch.uint8, device=gpu_device))
+    assert shaped[0].item() == k["shaped_total"]
+
+
+def test_notebook_mode_matches_oracle_over_episodes(gpu_device):
+    """Multi-frame: 2-back history, auto-reset restarts it, 300-step timeout."""
+    n, frames = 4099, 700
+    cfg = EnvConfig(randomize_drone=True, auto_reset=True, seed=12)
+    env = VecDroneEnv(n, device=gpu_device, config=cfg, precision="f64", reward_mode="notebook", max_steps=300)
+    env.reset()
+    o = ora.OracleEnv(n, precision="f64", config=cfg)
+    o.reset()
+    hist = np.full((2, n), np.nan)
+    hist[0] = host(env.shaped_hist)[0]
+    assert np.array_equal(hist[0], host(env.shaped_hist)[0])
+    rng = np.random.default_rng(3)
+    worst, timeouts = 0.0, 0
+    for t in range(frames):
+        a = rng.integers(0, 8, n).astype(np.uint8)
+        _, shaped, sdone, _ = env.step(torch.as_tensor(a, device=gpu_device))
+        *_, oshaped, osdone = o.step_shaped(a, hist, 300)
+        np.testing.assert_array_equal(host(sdone), osdone)
+        worst = max(worst, float(np.max(np.abs(host(shaped) - oshaped))))
+        timeouts += int(((host(env.steps) == 300) & host(sdone)).sum())
+    assert worst < 1e-9
+    assert timeouts > 0  # some episodes hit the 300-step cap

@@ -250,3 +250,34 @@ def test_oracle_sharding_invariance():
         np.testing.assert_array_equal(of, np.concatenate([oa, ob]))
         np.testing.assert_array_equal(rf, np.concatenate([ra, rb]))
     assert full.episode.max() > 1  # auto-reset happened
+
+
+def shaped_fixture_env(rec, precision="f64"):
+    n = rec["in_x"].shape[0]
+    env = ora.OracleEnv(n, precision=precision)
+    env.load_state_dict(gd.state_from_inputs(rec))
+    hist = np.full((2, n), np.nan)
+    slot = (rec["in_steps"].astype(np.int64) + 1) & 1  # the slot the frame reads
+    hist[slot, np.arange(n)] = rec["in_prev"]
+    return env, hist
+
+
+def test_oracle_notebook_reward_bit_exact():
+    """The notebooks' shaped reward + max_steps timeout."""
+    rec = gd.npz("shaped_reward.npz")
+    env, hist = shaped_fixture_env(rec)
+    obs, reward, done, obs64, shaped, sdone = env.step_shaped(rec["in_action"], hist, int(rec["max_steps"]))
+    np.testing.assert_array_equal(shaped, rec["out_shaped"])
+    np.testing.assert_array_equal(sdone, rec["out_shaped_done"])
+    # the history slot now holds this frame's distance
+    slot = (rec["in_steps"].astype(np.int64) + 1) & 1
+    np.testing.assert_array_equal(hist[slot, np.arange(len(slot))], obs64[:, 9])
+
+
+def test_oracle_notebook_reward_kat():
+    k = gd.js("kat_notebooks.json")["actor_critic_ppo"]
+    env = ora.OracleEnv(1, precision="f64")
+    env.load_state_dict(gd.edge_case_state({"state": gd.base_state(**k["start"])}))
+    hist = np.full((2, 1), np.nan)
+    *_, shaped, sdone = env.step_shaped([k["action"]], hist)
+    assert shaped[0] == k["shaped_total"]
