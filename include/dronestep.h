@@ -225,6 +225,17 @@ int64_t dd_compact_workspace(int64_t n);
 int dd_compact(const uint8_t *flags, int32_t want, int32_t *idx_out,
                int32_t *count, int32_t *workspace, int64_t n, void *stream);
 
+/* Generalised advantage estimation over a [T][N] rollout (compute_gae of
+ * Actor_Critic_PPO.ipynb:733-787, per lane; a done at t cuts the recursion):
+ *   delta = r[t] + gamma * v[t+1] * (1 - d[t]) - v[t]
+ *   gae   = delta + gamma * lambda * (1 - d[t]) * gae
+ * in float32 with the notebook's operation order (torch float32 tensors,
+ * Python-float gamma / lambda).  values is [T+1][N] (row T = bootstrap).
+ * returns (nullable) = advantages + values[t], as the notebook forms them. */
+int dd_gae(const float *rewards, const float *values, const uint8_t *dones,
+           float *advantages, float *returns, int64_t T, int64_t n,
+           double gamma, double lambda, void *stream);
+
 /* Algorithmic HBM bytes of one dd_step lane (the roofline byte model,
  * DESIGN.md §4): precision, action format, obs on/off. */
 int64_t dd_step_bytes_per_env(int32_t precision, int32_t action_format,

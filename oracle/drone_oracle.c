@@ -413,3 +413,26 @@ double ora_bench(const DDConfig *c, int64_t lane0, int64_t n, int64_t steps) {
     free(lanes);
     return sum;
 }
+
+/* compute_gae (Actor_Critic_PPO.ipynb:733-787) for every column of a
+ * [T][n] float32 rollout; torch float32 semantics: Python-float gamma is
+ * rounded to float32 where it meets a tensor, gamma * lambda_ is formed in
+ * double first. */
+void ora_gae(const float *rewards, const float *values, const uint8_t *dones, float *adv, int64_t T, int64_t n,
+             double gamma, double lambda) {
+    const float g = (float)gamma, gl = (float)(gamma * lambda);
+    for (int64_t i = 0; i < n; ++i) {
+        float gae = 0.0f;
+        for (int64_t t = T - 1; t >= 0; --t) {
+            float mask = 1.0f - (dones[t * n + i] ? 1.0f : 0.0f);
+            float a = g * values[(t + 1) * n + i];
+            a = a * mask;
+            float delta = rewards[t * n + i] + a;
+            delta = delta - values[t * n + i];
+            float b = gl * mask;
+            b = b * gae;
+            gae = delta + b;
+            adv[t * n + i] = gae;
+        }
+    }
+}

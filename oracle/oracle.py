@@ -56,6 +56,8 @@ def lib() -> ctypes.CDLL:
                 h.ora_philox4x32_10.argtypes = [P, P, P]
                 h.ora_philox4x32_10.restype = None
                 h.ora_bench.argtypes = [cfgp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
+                h.ora_gae.argtypes = [P, P, P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_double]
+                h.ora_gae.restype = None
                 h.ora_bench.restype = ctypes.c_double
                 _LIB = h
     return _LIB
@@ -167,6 +169,17 @@ class OracleEnv:
     def load_state_dict(self, d):
         for k, v in d.items():
             getattr(self, k)[:] = v
+
+
+def gae(rewards, values, dones, gamma=0.99, lam=0.95):
+    """compute_gae per column of [T, n] float32 arrays (values [T+1, n])."""
+    r = np.ascontiguousarray(rewards, dtype=np.float32)
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    d = np.ascontiguousarray(dones, dtype=np.uint8)
+    T, n = r.shape
+    adv = np.zeros((T, n), dtype=np.float32)
+    lib().ora_gae(_p(r), _p(v), _p(d), _p(adv), T, n, gamma, lam)
+    return adv
 
 
 def bench(config: EnvConfig, lane0: int, n: int, steps: int) -> float:

@@ -777,6 +777,33 @@ __global__ __launch_bounds__(kBlock) void info_kernel(Soa<T> a, T* distance, T* 
 }
 
 // ---------------------------------------------------------------------------
+// dd_gae: one lane per env walks its column of the [T][N] rollout backwards.
+// The loads of a frame do not depend on the running gae, so the compiler
+// keeps several frames' loads in flight (unroll 4).  Float32 throughout, in
+// compute_gae's order: torch evaluates `gamma * v` with gamma rounded to
+// float32 and `gamma * lambda_` in Python doubles before that rounding.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void gae_kernel(const float* rewards, const float* values, const uint8_t* dones,
+                                                     float* adv, float* ret, int32_t T, int64_t n, float g,
+                                                     float gl) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float gae = 0.0f;
+    float v_next = values[(int64_t)T * n + i];
+#pragma unroll 4
+    for (int32_t t = T - 1; t >= 0; --t) {
+        const int64_t o = (int64_t)t * n + i;
+        const float v = values[o];
+        const float mask = 1.0f - (float)dones[o];
+        const float delta = (rewards[o] + (g * v_next) * mask) - v;
+        gae = delta + (gl * mask) * gae;
+        __builtin_nontemporal_store(gae, adv + o);
+        if (ret) __builtin_nontemporal_store(gae + v, ret + o);
+        v_next = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Ordered compaction (dd_compact): count per tile -> exclusive scan of tile
 // counts -> scatter in lane order.  Ballots give each wave its count and each
 // lane its rank; LDS combines the block's four waves.
@@ -1062,6 +1089,19 @@ int dd_get_info(const DDConfig* cfg, const DDState* st, void* distance, void* sp
                                distance ? (double*)distance + first : nullptr,
                                speed ? (double*)speed + first : nullptr, len);
     }
+    return dd::finish();
+}
+
+int dd_gae(const float* rewards, const float* values, const uint8_t* dones, float* advantages, float* returns,
+           int64_t T, int64_t n, double gamma, double lambda, void* stream) {
+    if (T < 0 || n < 0 || T > INT32_MAX) return hipErrorInvalidValue;
+    if (T == 0 || n == 0) return 0;
+    if (!rewards || !values || !dones || !advantages) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const float g = (float)gamma;
+    const float gl = (float)(gamma * lambda);
+    hipLaunchKernelGGL(dd::gae_kernel, dim3((unsigned)dd::tiles_of(n)), dim3(dd::kBlock), 0, s, rewards, values,
+                       dones, advantages, returns, (int32_t)T, n, g, gl);
     return dd::finish();
 }
 

@@ -10,10 +10,11 @@ from .config import EnvConfig
 from .vec_env import OBS_KEYS, StepInfo, VecDroneEnv
 from .compat import DroneGame, DroneGameClient, DroneState, action_bits
 from .sharding import dist_env, gather_obs, shard_bounds
+from .gae import gae
 
 __all__ = [
     "EnvConfig", "VecDroneEnv", "StepInfo", "OBS_KEYS",
     "DroneGame", "DroneGameClient", "DroneState", "action_bits",
-    "shard_bounds", "dist_env", "gather_obs",
+    "shard_bounds", "dist_env", "gather_obs", "gae",
 ]
 __version__ = "0.1.0"

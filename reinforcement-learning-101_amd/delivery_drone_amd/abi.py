@@ -103,6 +103,8 @@ EXPORTS = {
                                     ctypes.c_int64, ctypes.c_void_p]),
     "dd_get_info": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "dd_gae": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]),
     "dd_compact_workspace": (ctypes.c_int64, [ctypes.c_int64]),
     "dd_compact": (ctypes.c_int, [ctypes.c_void_p, _I, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),

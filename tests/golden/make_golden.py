@@ -427,6 +427,34 @@ def shaped_set(rng, counts: dict, max_steps: int = 300) -> dict:
     return rec
 
 
+def gae_set(seed=5, T=257, cols=48, gamma=0.99, lam=0.95) -> dict:
+    """compute_gae of Actor_Critic_PPO.ipynb:733-787 (executed from the cell),
+    column by column, on CPU float32 torch tensors."""
+    import json as _json
+    import torch
+    nb = _json.load(open(os.path.join(REF, "Actor_Critic_PPO.ipynb")))
+    ns = {"torch": torch}
+    for cell in nb["cells"]:
+        src = "".join(cell["source"])
+        if cell["cell_type"] == "code" and "def compute_gae" in src:
+            exec(compile(src, "Actor_Critic_PPO.ipynb", "exec"), ns)
+    compute_gae = ns["compute_gae"]
+    rng = np.random.default_rng(seed)
+    rewards = rng.normal(0, 30, (T, cols)).astype(np.float32)
+    rewards[rng.random((T, cols)) < 0.05] = -300.0
+    values = rng.normal(0, 50, (T + 1, cols)).astype(np.float32)
+    dones = rng.random((T, cols)) < 0.02
+    dones[-1, ::3] = True
+    adv = np.zeros((T, cols), dtype=np.float32)
+    for j in range(cols):
+        a = compute_gae(rewards[:, j].tolist(), values[:, j], dones[:, j].tolist(), gamma=gamma, lambda_=lam,
+                        device=torch.device("cpu"))
+        adv[:, j] = a.numpy()
+    ret = (torch.from_numpy(adv) + torch.from_numpy(values[:T])).numpy()
+    return dict(rewards=rewards, values=values, dones=dones, advantages=adv, returns=ret,
+                gamma=np.float64(gamma), lam=np.float64(lam))
+
+
 def main():
     rng = np.random.default_rng(20261015)
     kats = notebook_kats()
@@ -455,6 +483,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "shaped_reward.npz"),
                         **shaped_set(np.random.default_rng(777), {"broad": 1200, "pad": 1200, "ground": 400,
                                                                  "bounds": 200}))
+    np.savez_compressed(os.path.join(HERE, "gae.npz"), **gae_set())
     print("fixtures written to", HERE)
 
 

@@ -139,3 +139,34 @@ def test_config5_shape_against_oracle(gpu_device):
         assert gd.f32_close(obs_h[t], oo, 1.0).all(), t
         assert gd.f32_close(rew_h[t], orr, 1.0).all(), t
     assert torch.isfinite(obs).all()
+
+
+def test_gae_vs_notebook(gpu_device):
+    """dd_gae against compute_gae's own outputs, bit for bit."""
+    from delivery_drone_amd import gae
+    g = gd.npz("gae.npz")
+    dev = gpu_device
+    adv, ret = gae(torch.as_tensor(g["rewards"], device=dev), torch.as_tensor(g["values"], device=dev),
+                   torch.as_tensor(g["dones"], device=dev), float(g["gamma"]), float(g["lam"]))
+    np.testing.assert_array_equal(adv.cpu().numpy(), g["advantages"])
+    np.testing.assert_array_equal(ret.cpu().numpy(), g["returns"])
+    # T-row values: bootstrap 0 appended, as compute_gae does
+    adv0 = gae(torch.as_tensor(g["rewards"], device=dev), torch.as_tensor(g["values"][:-1], device=dev),
+               torch.as_tensor(g["dones"], device=dev), returns=False)
+    want = ora.gae(g["rewards"], np.concatenate([g["values"][:-1], np.zeros((1, g["values"].shape[1]),
+                                                                             np.float32)]), g["dones"])
+    np.testing.assert_array_equal(adv0.cpu().numpy(), want)
+
+
+def test_gae_on_a_rollout_large(gpu_device):
+    """Config-5 shaped buffers straight from dd_rollout into dd_gae."""
+    from delivery_drone_amd import gae
+    n, k = 65_536, 256
+    env = VecDroneEnv(n, device=gpu_device, randomize_drone=True, auto_reset=True, seed=2)
+    env.reset()
+    obs, reward, done = env.rollout(frames=k)
+    values = torch.randn(k + 1, n, device=gpu_device)
+    adv, ret = gae(reward, values, done)
+    lo = n - 512
+    want = ora.gae(reward[:, lo:].cpu().numpy(), values[:, lo:].cpu().numpy(), done[:, lo:].cpu().numpy())
+    np.testing.assert_array_equal(adv[:, lo:].cpu().numpy(), want)

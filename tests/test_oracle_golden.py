@@ -281,3 +281,11 @@ def test_oracle_notebook_reward_kat():
     hist = np.full((2, 1), np.nan)
     *_, shaped, sdone = env.step_shaped([k["action"]], hist)
     assert shaped[0] == k["shaped_total"]
+
+
+def test_oracle_gae_bit_exact():
+    """compute_gae, float32, against the notebook's function."""
+    g = gd.npz("gae.npz")
+    adv = ora.gae(g["rewards"], g["values"], g["dones"], float(g["gamma"]), float(g["lam"]))
+    np.testing.assert_array_equal(adv, g["advantages"])
+    np.testing.assert_array_equal(adv + g["values"][:-1], g["returns"])
