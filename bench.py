@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--rollout-point", type=int, default=65_536,
                    help="also time BASELINE config 5 (this many envs x 256 frames via dd_rollout) at N=1 "
                         "and report it as rollout_point (0 = skip)")
+    p.add_argument("--no-extra-points", dest="extra_points", action="store_false",
+                   help="skip the notebook-reward point")
     p.add_argument("--hbm-point", type=int, default=16_777_216,
                    help="also time this many drones (HBM-resident) at N=1 and report it as hbm_point (0 = skip)")
     return p.parse_args()
@@ -191,6 +193,55 @@ def rollout_point(n, frames, precision, seed, dev):
     return out
 
 
+def gae_point(n, frames, dev):
+    """dd_gae over a [frames, n] rollout: reads reward,
+    value (+ bootstrap row), done; writes advantage and return."""
+    import torch
+    from delivery_drone_amd import gae
+    rew = torch.randn(frames, n, device=dev)
+    val = torch.randn(frames + 1, n, device=dev)
+    done = torch.rand(frames, n, device=dev) < 0.01
+    adv = torch.empty(frames, n, device=dev)
+    ret = torch.empty(frames, n, device=dev)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        gae(rew, val, done, out=(adv, ret))
+        torch.cuda.synchronize(dev)
+        reps = 20
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            gae(rew, val, done, out=(adv, ret))
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    nbytes = frames * n * (4 + 4 + 1 + 4 + 4) + n * 4
+    gbs = nbytes / (us * 1e-6) / 1e9
+    del rew, val, done, adv, ret
+    torch.cuda.empty_cache()
+    return {"envs": n, "frames": frames, "us": round(us, 2), "achieved": round(gbs, 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes": nbytes, "kernel": "dd::gae_kernel"}
+
+
+def notebook_point(n, precision, seed, dev):
+    """The step with the notebooks' reward fused:
+    reward_mode='notebook', max_steps=300, config-3 batch."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg, precision=precision, reward_mode="notebook", max_steps=300)
+    env.reset()
+    rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
+    ms = time_steps(env, rows, 500, 50, torch.cuda.Stream(dev))
+    bpe = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=True) + 8 + 8 + 4 + 1  # + hist r/w, shaped r, done
+    gbs = bpe * n / (ms * 1e-3) / 1e9
+    del env, rows
+    torch.cuda.empty_cache()
+    return {"envs": n, "us_per_step": round(ms * 1e3, 3), "steps_per_s": round(n / (ms * 1e-3), 1),
+            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env": bpe,
+            "kernel": "dd::step_kernel<float, 0, true, true, 1> (reward_mode='notebook')"}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -293,9 +344,12 @@ def main():
     hbm = None
     if world == 1 and args.hbm_point > 0:
         hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
-    c5 = None
+    c5 = g5 = nb = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
+        g5 = gae_point(args.rollout_point, 256, dev)
+    if world == 1 and args.extra_points:
+        nb = notebook_point(n, args.precision, args.seed, dev)
 
     if rank == 0:
         total_steps = n * world * args.steps
@@ -344,6 +398,8 @@ def main():
             "cpu_baseline": cpu,
             "hbm_point": hbm,
             "rollout_point": c5,
+            "gae_point": g5,
+            "notebook_reward_point": nb,
             "gpu_ms_per_step": round(step_ms, 6),
             "device": torch.cuda.get_device_name(dev),
         }

@@ -783,15 +783,40 @@ __global__ __launch_bounds__(kBlock) void info_kernel(Soa<T> a, T* distance, T* 
 // compute_gae's order: torch evaluates `gamma * v` with gamma rounded to
 // float32 and `gamma * lambda_` in Python doubles before that rounding.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void gae_kernel(const float* rewards, const float* values, const uint8_t* dones,
-                                                     float* adv, float* ret, int32_t T, int64_t n, float g,
+__global__ __launch_bounds__(kBlock) void gae_kernel(const float* __restrict__ rewards,
+                                                     const float* __restrict__ values,
+                                                     const uint8_t* __restrict__ dones, float* __restrict__ adv,
+                                                     float* __restrict__ ret, int32_t T, int64_t n, float g,
                                                      float gl) {
+    // Frames are processed in groups of kG: the group's loads are all issued
+    // before its (serial) arithmetic, so kG loads per array are in flight.
+    constexpr int kG = 8;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     float gae = 0.0f;
     float v_next = values[(int64_t)T * n + i];
-#pragma unroll 4
-    for (int32_t t = T - 1; t >= 0; --t) {
+    int32_t t = T - 1;
+    for (; t >= kG - 1; t -= kG) {
+        float r[kG], v[kG], d[kG];
+#pragma unroll
+        for (int j = 0; j < kG; ++j) {
+            const int64_t o = (int64_t)(t - j) * n + i;
+            r[j] = rewards[o];
+            v[j] = values[o];
+            d[j] = (float)dones[o];
+        }
+#pragma unroll
+        for (int j = 0; j < kG; ++j) {
+            const int64_t o = (int64_t)(t - j) * n + i;
+            const float mask = 1.0f - d[j];
+            const float delta = (r[j] + (g * v_next) * mask) - v[j];
+            gae = delta + (gl * mask) * gae;
+            __builtin_nontemporal_store(gae, adv + o);
+            if (ret) __builtin_nontemporal_store(gae + v[j], ret + o);
+            v_next = v[j];
+        }
+    }
+    for (; t >= 0; --t) {
         const int64_t o = (int64_t)t * n + i;
         const float v = values[o];
         const float mask = 1.0f - (float)dones[o];

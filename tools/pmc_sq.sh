@@ -20,7 +20,7 @@ for g in "${groups[@]}"; do
   [ -z "$sel" ] && continue
   for N in 262144 16777216; do
     S=$(( N > 1000000 ? 20 : 50 ))
-    timeout -k 10 300 rocprofv3 --pmc $sel --kernel-include-regex step_kernel -d $OUT/g${i}_$N -o pmc -f csv -- python3 bench.py --envs-per-gpu $N --steps $S --warmup 3 --graph-steps 0 --cpu-baseline 0 --hbm-point 0 --rollout-point 0 > /dev/null 2>> $OUT/err.log || { echo "group $i N $N failed"; exit 1; }
+    timeout -k 10 300 rocprofv3 --pmc $sel --kernel-include-regex step_kernel -d $OUT/g${i}_$N -o pmc -f csv -- python3 bench.py --envs-per-gpu $N --steps $S --warmup 3 --graph-steps 0 --cpu-baseline 0 --hbm-point 0 --rollout-point 0 --no-extra-points > /dev/null 2>> $OUT/err.log || { echo "group $i N $N failed"; exit 1; }
   done
   i=$((i+1))
 done
