@@ -170,3 +170,29 @@ def test_gae_on_a_rollout_large(gpu_device):
     lo = n - 512
     want = ora.gae(reward[:, lo:].cpu().numpy(), values[:, lo:].cpu().numpy(), done[:, lo:].cpu().numpy())
     np.testing.assert_array_equal(adv[:, lo:].cpu().numpy(), want)
+
+
+def test_rollout_wide_kernel_equals_step_loop(gpu_device):
+    """Above 262,144 lanes dd_rollout uses the one-lane-per-drone kernel
+    (below it, the lane-pair kernel the other tests cover)."""
+    n, k = 262_144 + 1037, 24
+    roll, loop = twins(n, gpu_device, "f32", randomize_drone=True, auto_reset=True, seed=13)
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
+    obs, reward, done = roll.rollout(acts)
+    for t in range(k):
+        o, r, d, _ = loop.step(acts[t])
+        assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
+    assert_same_state(roll, loop)
+
+
+@pytest.mark.parametrize("cfg", [dict(platform_moving=True), dict(wind_enabled=True, wind_x=0.05, wind_y=-0.02),
+                                 dict(auto_reset=False)])
+def test_pair_rollout_switches(cfg, gpu_device):
+    """Lane-pair kernel with the moving platform, wind and sticky done."""
+    roll, loop = twins(777, gpu_device, "f64", randomize_drone=True, seed=14, **cfg)
+    acts = torch.randint(0, 8, (80, 777), device=gpu_device, dtype=torch.uint8)
+    obs, reward, done = roll.rollout(acts)
+    for t in range(80):
+        o, r, d, _ = loop.step(acts[t])
+        assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
+    assert_same_state(roll, loop)
