@@ -718,158 +718,6 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
     if (live) store_spawn(a, i, s);  // every field: lanes may have re-spawned
 }
 
-// ---------------------------------------------------------------------------
-// Lane-pair rollout: two lanes share one drone.  At small batches (config 5:
-// 65,536 envs = one wave per SIMD) the frame's serial chain of double ops is
-// the bound, not bandwidth; splitting the frame's three independent costly
-// pieces over a lane pair halves that chain and doubles the waves:
-//   even lane: sincos(pre-update angle) (thrust), sqrt(speed^2), obs cols 0-6
-//   odd lane:  sincos(post-update angle) (bottom), sqrt(dist^2), obs cols 7-14
-// Partners trade results with one __shfl_xor(.., 1).  The arithmetic is the
-// same as frame() operation for operation, so results are identical.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double xchg(double v) { return __shfl_xor(v, 1); }
-
-__device__ __forceinline__ double frame_pair(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s, bool odd) {
-    const DDConfig& c = k.c;
-    const bool main_on = act & 1u, left_on = act & 2u, right_on = act & 4u;
-    // Drone.apply_thrust's fuel gating and rotation first (they do not read vx/vy)
-    const bool fire = main_on && s.fuel > 0.0;
-    double fuel = fire ? s.fuel - c.fuel_main : s.fuel;
-    double omega = s.omega;
-    if (left_on && fuel > 0.0) { omega -= c.side_thrust_power; fuel -= c.fuel_side; }
-    if (right_on && fuel > 0.0) { omega += c.side_thrust_power; fuel -= c.fuel_side; }
-    // the post-update angle depends on angle and omega only (Drone.update)
-    const double angle_post = trig::normalize_angle(s.angle + omega * c.dt);
-    double sl, cl;
-    sincos_deg(odd ? angle_post : s.angle, &sl, &cl);
-    const double so = xchg(sl), co = xchg(cl);
-    const double sa = odd ? so : sl, ca = odd ? co : cl;  // sin/cos of the pre-update angle
-    const double sb = odd ? sl : so, cb = odd ? cl : co;  // ... of the post-update angle
-    if (fire) {
-        const double ty = -c.main_thrust_power;
-        s.vx += 0.0 * ca - ty * sa;
-        s.vy += 0.0 * sa + ty * ca;
-    }
-    s.fuel = fuel > 0.0 ? fuel : 0.0;
-    if (sw.wind_enabled) { s.vx += sw.wind_x; s.vy += sw.wind_y; }
-    s.vy += c.gravity * c.dt;
-    s.vx *= c.drag;
-    s.vy *= c.drag;
-    s.x += s.vx * c.dt;
-    s.y += s.vy * c.dt;
-    s.omega = omega * c.angular_drag;
-    s.angle = angle_post;
-    if (sw.platform_moving) {
-        const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
-        s.px += c.platform_speed * dir * c.dt;
-        if (s.px <= c.platform_min_x) { s.px = c.platform_min_x; s.status &= ~DD_ST_PLAT_LEFT; }
-        else if (s.px >= c.platform_max_x) { s.px = c.platform_max_x; s.status |= DD_ST_PLAT_LEFT; }
-    }
-    const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
-    const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
-    const bool on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
-                        (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
-    {   // measure(): even lane the speed, odd lane the distance
-        const double dx = s.px - s.x, dy = s.py - s.y;
-        const double q = sqrt(odd ? dx * dx + dy * dy : s.vx * s.vx + s.vy * s.vy);
-        const double qo = xchg(q);
-        s.speed = odd ? qo : q;
-        s.dist = odd ? q : qo;
-    }
-    const bool slow = !(s.speed > c.max_landing_velocity);
-    const bool upright = fabs(s.angle) <= c.max_landing_angle;
-    const bool landing = on_pad & slow & upright;
-    const bool crash = s.y > c.ground_level;
-    const bool no_fuel = s.fuel <= 0.0;
-    const bool oob = (s.x < -c.oob_margin) | (s.x > c.world_width + c.oob_margin) |
-                     (s.y < -c.oob_margin) | (s.y > c.world_height + c.oob_margin);
-    double term = trig::div_exact(c.shaping_offset - s.dist, c.shaping_scale, k.inv_shaping);
-    term = oob ? c.reward_out_of_bounds : term;
-    term = no_fuel ? c.reward_out_of_fuel : term;
-    term = crash ? c.reward_crash : term;
-    term = landing ? c.reward_landing : term;
-    const bool terminal = landing | crash | no_fuel | oob;
-    s.status |= landing ? (DD_ST_LANDED | DD_ST_DONE) : terminal ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
-    const double reward = c.reward_step + term;
-    s.total += reward;
-    s.steps += 1;
-    return reward;
-}
-
-// get_state split over the pair: even lane columns 0-6, odd lane 7-14.
-__device__ __forceinline__ void observe_pair(const Consts& k, const Lane& s, bool odd, float* o) {
-    const DDConfig& c = k.c;
-    if (!odd) {
-        o[0] = (float)trig::div_exact(s.x, c.world_width, k.inv_w);
-        o[1] = (float)trig::div_exact(s.y, c.world_height, k.inv_h);
-        o[2] = (float)trig::div_exact(s.vx, c.vel_scale, k.inv_vel);
-        o[3] = (float)trig::div_exact(s.vy, c.vel_scale, k.inv_vel);
-        o[4] = (float)trig::div_exact(s.angle, c.angle_scale, k.inv_angle);
-        o[5] = (float)trig::div_exact(s.omega, c.vel_scale, k.inv_vel);
-        o[6] = (float)trig::div_exact(s.fuel, c.max_fuel, k.inv_fuel);
-    } else {
-        const double dx = s.px - s.x, dy = s.py - s.y;
-        o[7] = (float)trig::div_exact(s.px, c.world_width, k.inv_w);
-        o[8] = (float)trig::div_exact(s.py, c.world_height, k.inv_h);
-        o[9] = (float)trig::div_exact(s.dist, c.world_width, k.inv_w);
-        o[10] = (float)trig::div_exact(dx, c.world_width, k.inv_w);
-        o[11] = (float)trig::div_exact(dy, c.world_height, k.inv_h);
-        o[12] = (float)trig::div_exact(s.speed, c.vel_scale, k.inv_vel);
-        o[13] = (s.status & DD_ST_LANDED) ? 1.0f : 0.0f;
-        o[14] = (s.status & DD_ST_CRASHED) ? 1.0f : 0.0f;
-    }
-}
-
-constexpr int kPairRows = kBlock / 2;  // drones per block in the pair kernel
-
-template <typename T, int AFMT, bool kRef>
-__global__ __launch_bounds__(kBlock) void rollout_pair_kernel(RolloutArgs p, Soa<T> a) {
-    __shared__ __attribute__((aligned(16))) float tile[2][kPairRows * DD_OBS_DIM];
-    const DDConfig& sw = p.k.c;
-    const Consts& k = kRef ? kRefConsts : p.k;
-    const bool odd = threadIdx.x & 1u;
-    const uint32_t row0 = blockIdx.x * kPairRows;
-    const uint32_t r = threadIdx.x >> 1;
-    const uint32_t i = row0 + r;
-    const bool live = i < (uint32_t)p.n;  // same for both lanes of a pair
-    const int rows = (int)min((uint32_t)kPairRows, (uint32_t)p.n - row0);
-    const int64_t env = a.env_id_base + i;
-    Lane s;
-    uint32_t next = 0;
-    if (live) {
-        load_dynamics(a, i, s);
-        s.total = at(a.total, i);
-        s.status = at(a.status, i);
-        s.steps = at(a.steps, i);
-        s.episode = at(a.episode, i);
-        next = rollout_action<AFMT>(p, env, 0, i);
-    }
-    for (int f = 0; f < p.frames; ++f) {
-        const uint32_t act = next;
-        float* orow = tile[f & 1] + r * DD_OBS_DIM;
-        if (live) {
-            if (f + 1 < p.frames) next = rollout_action<AFMT>(p, env, f + 1, i);
-            double reward = 0.0;
-            if (s.status & DD_ST_DONE) {
-                if (sw.auto_reset) spawn(sw, env, s);  // both lanes: identical draws
-                else measure(s);
-            } else {
-                reward = frame_pair(k, sw, act, s, odd);
-            }
-            if (!odd) put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
-            else put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-            if (p.obs) observe_pair(k, s, odd, orow);
-            quantize<T>(s);
-        }
-        if (p.obs) {
-            __syncthreads();
-            flush_obs_tile(tile[f & 1], p.obs + ((size_t)f * p.n_total + row0) * DD_OBS_DIM, rows);
-        }
-    }
-    if (live && !odd) store_spawn(a, i, s);
-}
-
 // dd_shaped_reset kernel: the notebook reward's history restarts from the
 // current state (slot 0 = its distance, slot 1 = none).
 template <typename T>
@@ -1104,21 +952,9 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
     }
 }
 
-// Below ~4 waves per SIMD (256 CUs x 4 SIMDs x 4 waves x 64 lanes) the
-// rollout is bound by each frame's serial chain: split drones over lane pairs.
-// DD_ROLLOUT_PAIR_MAX_N overrides the switch point (A/B runs).
-#ifndef DD_ROLLOUT_PAIR_MAX_N
-#define DD_ROLLOUT_PAIR_MAX_N (256 * 4 * 4 * 64)
-#endif
-
 template <typename T, int AFMT, bool kRef>
 void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
-    if (p.n <= (int64_t)DD_ROLLOUT_PAIR_MAX_N) {
-        const unsigned blocks = (unsigned)((p.n + kPairRows - 1) / kPairRows);
-        hipLaunchKernelGGL((rollout_pair_kernel<T, AFMT, kRef>), dim3(blocks), dim3(kBlock), 0, s, p, a);
-    } else {
-        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
-    }
+    hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
 }
 
 template <typename T, bool kRef>

@@ -172,9 +172,8 @@ def test_gae_on_a_rollout_large(gpu_device):
     np.testing.assert_array_equal(adv[:, lo:].cpu().numpy(), want)
 
 
-def test_rollout_wide_kernel_equals_step_loop(gpu_device):
-    """Above 262,144 lanes dd_rollout uses the one-lane-per-drone kernel
-    (below it, the lane-pair kernel the other tests cover)."""
+def test_rollout_large_ragged_equals_step_loop(gpu_device):
+    """More lanes than one 2^18-lane wave of blocks, ragged tail."""
     n, k = 262_144 + 1037, 24
     roll, loop = twins(n, gpu_device, "f32", randomize_drone=True, auto_reset=True, seed=13)
     acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
@@ -187,8 +186,8 @@ def test_rollout_wide_kernel_equals_step_loop(gpu_device):
 
 @pytest.mark.parametrize("cfg", [dict(platform_moving=True), dict(wind_enabled=True, wind_x=0.05, wind_y=-0.02),
                                  dict(auto_reset=False)])
-def test_pair_rollout_switches(cfg, gpu_device):
-    """Lane-pair kernel with the moving platform, wind and sticky done."""
+def test_rollout_switches(cfg, gpu_device):
+    """dd_rollout with the moving platform, wind and sticky done (f64 storage)."""
     roll, loop = twins(777, gpu_device, "f64", randomize_drone=True, seed=14, **cfg)
     acts = torch.randint(0, 8, (80, 777), device=gpu_device, dtype=torch.uint8)
     obs, reward, done = roll.rollout(acts)
