@@ -404,6 +404,7 @@ __device__ __forceinline__ E& at(E* base, uint32_t i) {
 // DD_PLAIN_OUT_STORES restores plain stores for A/B runs.
 template <typename E>
 __device__ __forceinline__ void put_out(E* base, uint32_t i, E v) {
+    asm volatile("" : "+v"(i));  // keep the offset 32-bit and local: SGPR-base store
 #ifdef DD_PLAIN_OUT_STORES
     at(base, i) = v;
 #else
@@ -529,6 +530,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     s.status = r.status;
     s.steps = r.steps;
     bool ended = false;
+    bool respawned = false;
     double reward;
     double shaped = 0.0;
     bool shaped_done = false;
@@ -537,7 +539,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
         if (sw.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
             s.episode = at(a.episode, i);
             spawn(sw, a.env_id_base + i, s);
-            store_spawn(a, i, s);
+            respawned = true;
             if constexpr (kShaped) {  // the notebook's history restarts: prev_state None
                 at(p.shaped_hist, i) = trig::div_exact(s.dist, k.c.world_width, k.inv_w);
                 at(p.shaped_hist + p.hist_stride, i) = __builtin_nan("");
@@ -570,11 +572,22 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
             if (p.obs) write_obs_row(v, s.status, orow);
         }
         ended = (s.status & DD_ST_DONE) != 0;
-        store_dynamics(a, i, s);
-        if (sw.platform_moving) { at(a.px, i) = (T)s.px; at(a.status, i) = (uint8_t)s.status; }
-        else if (ended) at(a.status, i) = (uint8_t)s.status;
-        at(a.steps, i) = s.steps;
-        at(a.total, i) = (T)s.total;
+    }
+    // State stores after the branches merge, so each is one SGPR-base +
+    // lane-offset store (stores inside the branches got 64-bit per-lane
+    // addresses, 22 VGPRs live across the frame).  A sticky-done lane
+    // writes nothing; status and px only change on the terminal frame, a
+    // respawn or a moving platform; py and episode only on a respawn.
+    const bool sticky = (r.status & DD_ST_DONE) && !respawned;
+    if (!sticky) {
+        uint32_t j = i;
+        asm volatile("" : "+v"(j));  // an offset defined in this block: isel folds it into saddr stores
+        store_dynamics(a, j, s);
+        at(a.steps, j) = s.steps;
+        at(a.total, j) = (T)s.total;
+        if (sw.platform_moving || respawned) at(a.px, j) = (T)s.px;
+        if (sw.platform_moving || ended || respawned) at(a.status, j) = (uint8_t)s.status;
+        if (respawned) { at(a.py, j) = (T)s.py; at(a.episode, j) = s.episode; }
     }
     put_out(static_cast<T*>(p.reward), i, (T)reward);
     put_out(p.done, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
