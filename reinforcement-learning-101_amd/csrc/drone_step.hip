@@ -263,16 +263,28 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         else if (s.px >= c.platform_max_x) { s.px = c.platform_max_x; s.status |= DD_ST_PLAT_LEFT; }
     }
 
-    // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
-    double sb, cb;
-    sincos_deg(s.angle, &sb, &cb);
-    const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
-    const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
-    const bool on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
-                        (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
     measure(s);  // speed (get_speed) and distance (physics.distance), shared with get_state
     const bool slow = !(s.speed > c.max_landing_velocity);
     const bool upright = fabs(s.angle) <= c.max_landing_angle;
+
+    // get_bottom_center: rotate_point(0, height / 2, angle) on the updated
+    // angle.  It only matters through on_pad, and the bottom centre lies
+    // within |half_height| (+ rounding) of (x, y), so the rotation (the
+    // frame's second sincos) runs only for slow, upright drones within that
+    // reach of the pad; every other lane has on_pad = false exactly as the
+    // reference's comparisons would give (NaN fails both tests alike).
+    bool on_pad = false;
+    const double rx = c.platform_half_width + fabs(c.drone_half_height);
+    const double ry = c.platform_half_height + fabs(c.drone_half_height);
+    const double slack = 1.0 + 1e-9 * (fabs(s.x) + fabs(s.y) + fabs(s.px) + fabs(s.py) + rx + ry);
+    if (slow && upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack) {
+        double sb, cb;
+        sincos_deg(s.angle, &sb, &cb);
+        const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
+        const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
+        on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
+                 (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
+    }
 
     // _calculate_reward's cascade, evaluated branch-free: every predicate is
     // formed, then the first that holds picks the term.  (The nested
@@ -438,6 +450,7 @@ __device__ __forceinline__ void store_spawn(const Soa<T>& a, uint32_t i, const L
 // Writes a block's [rows, 15] observation tile from LDS to global memory as
 // 16-byte stores (non-temporal: the rows are the step's output stream, read
 // by the consumer, not by this kernel again).  dst = first row of the tile.
+template <int NB = kBlock>
 __device__ __forceinline__ void flush_obs_tile(const float* tile, float* dst, int rows) {
     const int nf = rows * DD_OBS_DIM;
     // tiles start at multiples of 256 rows (15360 B): dst is 16-B aligned iff obs is
@@ -445,17 +458,38 @@ __device__ __forceinline__ void flush_obs_tile(const float* tile, float* dst, in
         const int nv = nf >> 2;
         const f32x4* src4 = reinterpret_cast<const f32x4*>(tile);
         f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
-        for (int k = threadIdx.x; k < nv; k += kBlock) {
+        for (int k = threadIdx.x; k < nv; k += NB) {
 #ifdef DD_PLAIN_OBS_STORES
             dst4[k] = src4[k];
 #else
             __builtin_nontemporal_store(src4[k], &dst4[k]);
 #endif
         }
-        for (int k = (nv << 2) + threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
+        for (int k = (nv << 2) + threadIdx.x; k < nf; k += NB) dst[k] = tile[k];
     } else {
-        for (int k = threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
+        for (int k = threadIdx.x; k < nf; k += NB) dst[k] = tile[k];
     }
+}
+
+// The same for one wave's slice of the tile (rows <= 64, starting at the
+// wave's first row): only this wave wrote and reads the slice, so a
+// wave-level sync stands in for the block barrier and each wave's rows leave
+// as soon as its own lanes are done.  dst + 64-row slices of 3840 B keep
+// the 16-byte alignment of the tile.
+__device__ __forceinline__ void flush_obs_wave(const float* wtile, float* dst, int rows) {
+    __syncwarp();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nf = rows * DD_OBS_DIM;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+        const int nv = nf >> 2;
+        const f32x4* src4 = reinterpret_cast<const f32x4*>(wtile);
+        f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
+        for (int k = lane; k < nv; k += kWave) __builtin_nontemporal_store(src4[k], &dst4[k]);
+        for (int k = (nv << 2) + lane; k < nf; k += kWave) dst[k] = wtile[k];
+    } else {
+        for (int k = lane; k < nf; k += kWave) dst[k] = wtile[k];
+    }
+    __syncwarp();  // the slice may be rewritten next (rollout frames)
 }
 
 template <int AFMT>
@@ -494,9 +528,10 @@ struct StepArgs {
 #ifndef DD_STEP_MIN_WAVES
 #define DD_STEP_MIN_WAVES 1  // per SIMD; experiments raise it to force fewer VGPRs
 #endif
-#ifndef DD_LPT
-#define DD_LPT 1  // drones per thread (sub-tiles of 256 lanes per block)
+#ifndef DD_STEP_BLOCK
+#define DD_STEP_BLOCK 256  // lanes (= drones) per step block; experiments try 512 / 1024
 #endif
+constexpr int kStepBlock = DD_STEP_BLOCK;
 
 // A lane's inputs as loaded (storage width), before widening to double.
 template <typename T>
@@ -601,51 +636,43 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     return ended;
 }
 
-// dd_step kernel.  A block owns LPT consecutive 256-lane sub-tiles; each
-// thread loads its LPT lanes first, then finishes them one after the other,
-// so one sub-tile's stores and obs flush overlap the next one's arithmetic.
-template <typename T, int AFMT, bool kRef, bool kShaped, int LPT>
-__global__ __launch_bounds__(kBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
-    __shared__ __attribute__((aligned(16))) float tile[LPT][kBlock * DD_OBS_DIM];
-    const uint32_t base = blockIdx.x * (kBlock * LPT);
-    Raw<T> r[LPT];
-#pragma unroll
-    for (int j = 0; j < LPT; ++j) {
-        const uint32_t i = base + j * kBlock + threadIdx.x;
-        if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r[j]);
+// dd_step kernel: one drone per lane, one tile of kStepBlock lanes per block.
+template <typename T, int AFMT, bool kRef, bool kShaped>
+__global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
+#ifdef DD_EXP_EMPTY  // timing-only: the launch and dispatch floor
+    if (p.n >= 0) return;
+#endif
+    __shared__ __attribute__((aligned(16))) float tile[kStepBlock * DD_OBS_DIM];
+    const uint32_t row0 = blockIdx.x * kStepBlock;
+    const uint32_t i = row0 + threadIdx.x;
+    Raw<T> r;
+    if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r);
+    const bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM);
+    if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
+        const uint64_t m = __ballot(ended);
+        if (m) {
+            const int lane = threadIdx.x & (kWave - 1);
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            int b = 0;
+            if (lane == leader) b = atomicAdd(p.done_count, __popcll(m));
+            b = __shfl(b, leader);
+            if (ended) p.done_idx[b + before] = p.idx_base + (int32_t)i;
+        }
     }
-#pragma unroll
-    for (int j = 0; j < LPT; ++j) {
-        const uint32_t row0 = base + j * kBlock;
-        const uint32_t i = row0 + threadIdx.x;
-        const bool ended =
-            i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r[j], tile[j] + threadIdx.x * DD_OBS_DIM);
-        if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
-            const uint64_t m = __ballot(ended);
-            if (m) {
-                const int lane = threadIdx.x & (kWave - 1);
-                const int leader = __ffsll((unsigned long long)m) - 1;
-                const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                int b = 0;
-                if (lane == leader) b = atomicAdd(p.done_count, __popcll(m));
-                b = __shfl(b, leader);
-                if (ended) p.done_idx[b + before] = p.idx_base + (int32_t)i;
-            }
-        }
-        if (p.obs && row0 < (uint32_t)p.n) {  // uniform: the sub-tile leaves as 16-byte stores
-            __syncthreads();
-            const int rows = (int)min((uint32_t)kBlock, (uint32_t)p.n - row0);
-            flush_obs_tile(tile[j], p.obs + (size_t)row0 * DD_OBS_DIM, rows);
-        }
+    if (p.obs) {  // each wave's 64 rows leave as 16-byte stores
+        const uint32_t wrow0 = row0 + (threadIdx.x & ~(kWave - 1));
+        const int rows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
+        flush_obs_wave(tile + (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM, p.obs + (size_t)wrow0 * DD_OBS_DIM, rows);
     }
 }
 
 // ---------------------------------------------------------------------------
 // dd_rollout kernel: `frames` consecutive frames per launch, the lane's state
 // in registers between frames.  Per frame a lane reads its action (1 B, the
-// next frame's prefetched) and writes reward, done and its obs row (LDS tile,
-// double-buffered so one barrier per frame suffices).  Same frame code as
+// next frame's prefetched) and writes reward, done and its obs row (through
+// its wave's LDS slice; no block barrier, waves drift freely).  Same frame code as
 // step_kernel, so a rollout equals `frames` dd_step calls bit for bit.
 // ---------------------------------------------------------------------------
 struct RolloutArgs {
@@ -688,13 +715,16 @@ __device__ __forceinline__ void quantize(Lane& s) {
 
 template <typename T, int AFMT, bool kRef>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a) {
-    __shared__ __attribute__((aligned(16))) float tile[2][kBlock * DD_OBS_DIM];
+    __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     const uint32_t row0 = blockIdx.x * kBlock;
     const uint32_t i = row0 + threadIdx.x;
     const bool live = i < (uint32_t)p.n;
-    const int rows = (int)min((uint32_t)kBlock, (uint32_t)p.n - row0);
+    const uint32_t wrow0 = row0 + (threadIdx.x & ~(kWave - 1));  // this wave's first row
+    const int wrows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
+    const float* wtile = tile + (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM;
+    float* orow = tile + threadIdx.x * DD_OBS_DIM;
     const int64_t env = a.env_id_base + i;
     Lane s;
     uint32_t next = 0;
@@ -708,7 +738,6 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
     }
     for (int f = 0; f < p.frames; ++f) {
         const uint32_t act = next;
-        float* orow = tile[f & 1] + threadIdx.x * DD_OBS_DIM;
         if (live) {
             if (f + 1 < p.frames) next = rollout_action<AFMT>(p, env, f + 1, i);
             double reward = 0.0;
@@ -723,10 +752,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
             if (p.obs) observe(k, s, orow);
             quantize<T>(s);  // the obs above sees the unrounded frame, like dd_step's
         }
-        if (p.obs) {  // uniform: all threads run every frame
-            __syncthreads();
-            flush_obs_tile(tile[f & 1], p.obs + ((size_t)f * p.n_total + row0) * DD_OBS_DIM, rows);
-        }
+        if (p.obs) flush_obs_wave(wtile, p.obs + ((size_t)f * p.n_total + wrow0) * DD_OBS_DIM, wrows);
     }
     if (live) store_spawn(a, i, s);  // every field: lanes may have re-spawned
 }
@@ -923,8 +949,8 @@ bool state_ok(const DDState* st) {
 
 template <typename T, int AFMT, bool kRef, bool kShaped>
 void launch_step(const StepArgs& p, const Soa<T>& a, hipStream_t s) {
-    const unsigned blocks = (unsigned)((p.n + kBlock * DD_LPT - 1) / (kBlock * DD_LPT));
-    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShaped, DD_LPT>), dim3(blocks), dim3(kBlock), 0, s, p, a);
+    const unsigned blocks = (unsigned)((p.n + kStepBlock - 1) / kStepBlock);
+    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShaped>), dim3(blocks), dim3(kStepBlock), 0, s, p, a);
 }
 
 template <typename T, bool kRef, bool kShaped>

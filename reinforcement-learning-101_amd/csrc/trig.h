@@ -83,12 +83,12 @@ DD_HD inline void sincos(double x, double* s, double* c) {
     const double y1 = (r - y0) - w;
     const double sv = ksin(y0, y1);
     const double cv = kcos(y0, y1);
-    switch (n & 3) {
-        case 0: *s = sv; *c = cv; break;
-        case 1: *s = cv; *c = -sv; break;
-        case 2: *s = -sv; *c = -cv; break;
-        default: *s = -cv; *c = sv; break;
-    }
+    // quadrant n & 3 -> (sv, cv), (cv, -sv), (-sv, -cv), (-cv, sv), as
+    // selects and sign flips rather than a divergent switch
+    const double a = (n & 1) ? cv : sv;
+    const double b = (n & 1) ? sv : cv;
+    *s = (n & 2) ? -a : a;
+    *c = ((n + 1) & 2) ? -b : b;
 }
 
 // x / d, correctly rounded, in three double ops instead of the ~10 of the

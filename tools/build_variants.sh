@@ -22,9 +22,11 @@ for v in ${VARIANTS:-base}; do
     nofma) build nofma -DDD_TRIG_NO_FMA ;;
     plainout) build plainout -DDD_PLAIN_OUT_STORES ;;
     nomath) build nomath -DDD_EXP_NOMATH ;;
-    lpt2) build lpt2 -DDD_LPT=2 ;;
     obsmul) build obsmul -DDD_OBS_MUL ;;
-    lpt4) build lpt4 -DDD_LPT=4 ;;
+    empty) build empty -DDD_EXP_EMPTY ;;
+    b512) build b512 -DDD_STEP_BLOCK=512 ;;
+    b1024) build b1024 -DDD_STEP_BLOCK=1024 ;;
+    b128) build b128 -DDD_STEP_BLOCK=128 ;;
     w8) build w8 -DDD_STEP_MIN_WAVES=8 ;;
     w4) build w4 -DDD_STEP_MIN_WAVES=4 ;;
     *) echo "unknown variant $v" >&2; exit 1 ;;
