@@ -239,7 +239,7 @@ def notebook_point(n, precision, seed, dev):
     torch.cuda.empty_cache()
     return {"envs": n, "us_per_step": round(ms * 1e3, 3), "steps_per_s": round(n / (ms * 1e-3), 1),
             "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env": bpe,
-            "kernel": "dd::step_kernel<float, 0, true, true, 1> (reward_mode='notebook')"}
+            "kernel": "dd::step_kernel<float, 0, true, true> (reward_mode='notebook')"}
 
 
 def main():
@@ -365,7 +365,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(n, args.precision, write_obs),
             "bytes_per_env": bytes_env,
-            "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, 1>",
+            "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, false>",
             "timing": "HIP events on the launch stream over the K timed steps / K",
         }
         out = {
