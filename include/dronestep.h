@@ -10,6 +10,14 @@
  *   DroneGame._get_info game_engine.py:281-298 -> dd_get_info
  *   config.py:17-68 module constants           -> DDConfig (dd_config_default)
  *
+ * and for the notebooks' side of the loop:
+ *
+ *   calc_reward + max_steps  Actor_Critic_PPO.ipynb:164-263, :886-888 -> dd_step (shaped_*)
+ *   the collection loop       Actor_Critic_PPO.ipynb:797-917          -> dd_rollout
+ *   DroneGamerBoi / DroneTeacherBoi + Bernoulli.sample / log_prob
+ *                             Actor_Critic_PPO.ipynb:376-424, :851-859 -> dd_mlp_forward
+ *   compute_gae               Actor_Critic_PPO.ipynb:733-787          -> dd_gae
+ *
  * One call processes a batch of N independent drones stored as a
  * struct-of-arrays (SoA) in device memory.  The reference has no FFI of its
  * own (it is 100 % Python and its only cross-process surface is the JSON
@@ -36,7 +44,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 2
+#define DD_ABI_VERSION 3
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -235,6 +243,49 @@ int dd_compact(const uint8_t *flags, int32_t want, int32_t *idx_out,
 int dd_gae(const float *rewards, const float *values, const uint8_t *dones,
            float *advantages, float *returns, int64_t T, int64_t n,
            double gamma, double lambda, void *stream);
+
+/* ---- Policy and value networks ------------------
+ * The notebooks' DroneGamerBoi (actor) and DroneTeacherBoi (critic),
+ * Actor_Critic_PPO.ipynb:376-424:
+ *   Linear(15,128) LayerNorm(128) ReLU  Linear(128,128) LayerNorm(128) ReLU
+ *   Linear(128,64) LayerNorm(64) ReLU   Linear(64,K)  [+ Sigmoid, actor]
+ * with K = 3 (main, left, right) for the actor and K = 1 for the critic, in
+ * float32.  The parameters are the state_dict tensors (torch layout: weight
+ * [out][in] row-major, device pointers), repacked once by dd_mlp_pack into
+ * the kernel's MFMA operand order. */
+typedef struct DDMlpParams {
+    const float *w0, *b0, *ln1_w, *ln1_b; /* network.0 (Linear), network.1 (LayerNorm) */
+    const float *w3, *b3, *ln4_w, *ln4_b; /* network.3, network.4 */
+    const float *w6, *b6, *ln7_w, *ln7_b; /* network.6, network.7 */
+    const float *w9, *b9;                 /* network.9: [K][64], [K] */
+    int32_t out_dim;                      /* K: 3 (actor) or 1 (critic) */
+    float ln_eps;                         /* nn.LayerNorm eps (1e-5) */
+} DDMlpParams;
+
+/* One forward pass over N observation rows.  The actor (K = 3) writes the
+ * Sigmoid probabilities, and optionally samples actions as
+ * Bernoulli(probs).sample() (Actor_Critic_PPO.ipynb:857-858: bit j set iff
+ * u_j < p_j, u_j uniform in [0,1) from Philox4x32-10 keyed by
+ * (seed; env_id_base + i, step, 0x5A5A5A5A)) packed as the dd_step bitmask,
+ * with Bernoulli.log_prob(actions).sum(-1) (:859).  The critic (K = 1)
+ * writes the value. */
+typedef struct DDMlpIO {
+    const float *obs;    /* [N][15] f32, dd_step / dd_write_obs rows */
+    float *out;          /* nullable: [N][3] probabilities (actor) or [N] values (critic) */
+    uint8_t *actions;    /* actor, nullable: uint8 [N] sampled bitmask */
+    float *log_prob;     /* actor, nullable: [N] summed log-probability of `actions` */
+    uint64_t seed;
+    int64_t step;
+    int64_t env_id_base;
+} DDMlpIO;
+
+/* Floats of a packed parameter buffer (same for K = 1 and 3). */
+int64_t dd_mlp_packed_floats(void);
+/* Repack state_dict tensors into `packed` (device, dd_mlp_packed_floats()). */
+int dd_mlp_pack(const DDMlpParams *params, float *packed, void *stream);
+/* Forward pass; out_dim must match the packed parameters. */
+int dd_mlp_forward(const float *packed, int32_t out_dim, const DDMlpIO *io,
+                   int64_t n, void *stream);
 
 /* Algorithmic HBM bytes of one dd_step lane (the roofline byte model,
  * DESIGN.md §4): precision, action format, obs on/off. */

@@ -23,6 +23,7 @@
 #include <type_traits>
 
 #include "dronestep.h"
+#include "philox.h"
 #include "trig.h"
 
 namespace dd {
@@ -142,30 +143,6 @@ inline bool uses_reference_physics(const DDConfig& c) {
         if (memcmp(a + j, b + j, sizeof(double)) != 0) return false;
     }
     return true;
-}
-
-// ---------------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al., SC'11).  Spawn draws are keyed by
-// (seed; global env id, episode) so a lane's spawn is independent of how the
-// batch is sharded across ranks and of the launch geometry.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
-                                              uint32_t c3, uint32_t k0, uint32_t k1,
-                                              uint32_t out[4]) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-        c1 = (uint32_t)p1;
-        c3 = (uint32_t)p0;
-        c0 = n0;
-        c2 = n2;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
 // Uniform integer in [lo, lo + span) from one 32-bit draw (multiply-high).

@@ -1,0 +1,33 @@
+// philox.h — Philox4x32-10 (Salmon et al., SC'11), the counter-based
+// generator behind every random draw on the device: spawns are keyed by
+// (seed; global env id, episode, 0), in-kernel random actions by
+// (seed; env id, step, 0xA5A5A5A5 ^ step_hi), policy samples by
+// (seed; env id, step, 0x5A5A5A5A ^ step_hi).  Keyed by the global env id, a
+// lane's draws do not depend on sharding or launch geometry.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dd {
+
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
+                                              uint32_t c3, uint32_t k0, uint32_t k1,
+                                              uint32_t out[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+}  // namespace dd

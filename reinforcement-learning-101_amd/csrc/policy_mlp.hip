@@ -1,0 +1,315 @@
+// policy_mlp.hip — the notebooks' policy and value networks on gfx950 MFMA.
+//
+// DroneGamerBoi / DroneTeacherBoi (reference Actor_Critic_PPO.ipynb:376-424):
+//   Linear(15,128) LayerNorm ReLU  Linear(128,128) LayerNorm ReLU
+//   Linear(128,64) LayerNorm ReLU  Linear(64,K)  [Sigmoid for the actor]
+// plus the collection loop's Bernoulli(probs).sample() and
+// .log_prob(actions).sum(dim=1) (:851-859), for N observation rows per call.
+//
+// Shape of the work: 26.6k multiply-adds per row against 111 KB of weights
+// shared by every row, i.e. three small GEMMs per 32-row tile.  They run on
+// v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate, exact fmaf chains; 157 TF
+// dense, the same rate as the f32 VALU): the notebook's model is float32 and
+// the kernel keeps its precision.
+//
+//   * The activations are kept TRANSPOSED (hidden x drones): a wave owns 32
+//     drones (the MFMA's N) and each layer is out^T = W . in^T.  A 32x32
+//     accumulator tile holds hidden row (r&3) + 8(r>>2) + 4h of column
+//     lane&31 in register r (h = lane>>5), which is exactly the B-operand
+//     slot of the next layer's k-step (t, r) for k = that row.  So layer to
+//     layer the activations never leave the registers; the k order this
+//     implies is folded into the weights when they are packed.
+//   * LayerNorm of a drone's column reduces over its 128 (64) rows: 64 (32)
+//     per lane, then one cross-half shuffle.
+//   * The packed weights (A operands in MFMA lane order, 16 B per lane per
+//     4 k-steps so one ds_read_b128 feeds four MFMAs) live in LDS, loaded
+//     once per block of 8 waves (2 per SIMD, 1 block per CU).
+//   * The last layer (64 -> K <= 3) and the sampling run on the VALU.
+
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "dronestep.h"
+#include "philox.h"
+
+namespace dd {
+namespace mlp {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kIn = DD_OBS_DIM;  // 15
+constexpr int kWaves = 8;
+constexpr int kThreads = kWaves * 64;
+constexpr int kCols = 32;  // drones per wave tile
+
+// k-steps of 2 per layer (K = 16 for the 15 inputs + one zero column).
+constexpr int kSteps1 = 8, kSteps2 = 64, kSteps3 = 64;
+// Packed buffer (floats).  A sections are [out tile][k-step group of 4][lane][4].
+constexpr int kA1 = 0;
+constexpr int kA2 = kA1 + 4 * kSteps1 * 64;
+constexpr int kA3 = kA2 + 4 * kSteps2 * 64;
+constexpr int kV1 = kA3 + 2 * kSteps3 * 64;  // bias, LN weight, LN bias [3][128]
+constexpr int kV2 = kV1 + 3 * 128;
+constexpr int kV3 = kV2 + 3 * 128;  // [3][64]
+constexpr int kW4 = kV3 + 3 * 64;   // last layer [3][64], rows >= K zero
+constexpr int kB4 = kW4 + 3 * 64;   // bias [3], LayerNorm eps
+constexpr int kPacked = kB4 + 4;
+constexpr size_t kLdsBytes = kPacked * sizeof(float);
+static_assert(kPacked % 4 == 0, "packed buffer is read as float4");
+
+// Hidden row held in register r of accumulator tile t by lane half h
+// (C/D map of the 32x32 MFMAs on gfx950: row = (r&3) + 8(r>>2) + 4h).
+__host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// One packed float: which state_dict element (or zero) goes at index i.
+__global__ void pack_kernel(DDMlpParams p, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kPacked) return;
+    float v = 0.0f;
+    if (i < kV1) {  // A operands: lane l of k-step q of out tile t holds W[32t + (l&31)][k(q, l>>5)]
+        const int base = i < kA2 ? kA1 : i < kA3 ? kA2 : kA3;
+        const int steps = i < kA2 ? kSteps1 : i < kA3 ? kSteps2 : kSteps3;
+        const int o = i - base;
+        const int j = o & 3, l = (o >> 2) & 63, grp = o >> 8;
+        const int t = grp / (steps / 4), q = 4 * (grp % (steps / 4)) + j;
+        const int row = 32 * t + (l & 31), h = l >> 5;
+        if (base == kA1) {  // layer 1: natural k order, column 15 is zero
+            const int col = 2 * q + h;
+            v = col < kIn ? p.w0[row * kIn + col] : 0.0f;
+        } else {  // layers 2, 3: k-step (t', r) = q takes hidden row hid(t', r, h)
+            const int col = hid(q >> 4, q & 15, h);
+            v = (base == kA2 ? p.w3 : p.w6)[row * 128 + col];
+        }
+    } else if (i < kV2) {
+        const int o = i - kV1;
+        const float* src[3] = {p.b0, p.ln1_w, p.ln1_b};
+        v = src[o / 128][o % 128];
+    } else if (i < kV3) {
+        const int o = i - kV2;
+        const float* src[3] = {p.b3, p.ln4_w, p.ln4_b};
+        v = src[o / 128][o % 128];
+    } else if (i < kW4) {
+        const int o = i - kV3;
+        const float* src[3] = {p.b6, p.ln7_w, p.ln7_b};
+        v = src[o / 64][o % 64];
+    } else if (i < kB4) {
+        const int o = i - kW4;
+        v = (o / 64) < p.out_dim ? p.w9[o] : 0.0f;
+    } else {
+        const int o = i - kB4;
+        v = o < p.out_dim ? p.b9[o] : (o == 3 ? p.ln_eps : 0.0f);
+    }
+    out[i] = v;
+}
+
+// out^T tiles (NT of 32 rows) += W . in^T over STEPS k-steps; bval(q) is the
+// lane's B operand (its column's input at the k of step q).
+template <int NT, int STEPS, typename BVal>
+__device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lane, BVal bval, f32x16 (&acc)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+#pragma unroll
+    for (int g = 0; g < STEPS / 4; ++g) {
+        f32x4 a[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) a[t] = a4[(t * (STEPS / 4) + g) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float b = bval(4 * g + j);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][j], b, acc[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep each group's LDS reads next to its MFMAs
+    }
+}
+
+// + bias, LayerNorm over the column's 32*NT rows (biased variance, as
+// nn.LayerNorm), ReLU.  vec = [bias | weight | bias] of 32*NT each.
+template <int NT>
+__device__ __forceinline__ void bias_norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
+                                               float (&y)[NT][16]) {
+    constexpr int kRows = 32 * NT;
+    const float* bias = vec + 4 * h;
+    const float* gamma = vec + kRows + 4 * h;
+    const float* beta = vec + 2 * kRows + 4 * h;
+    float sum = 0.0f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            y[t][r] = acc[t][r] + bias[hid(t, r, 0)];
+            sum += y[t][r];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum / (float)kRows;
+    float sq = 0.0f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float d = y[t][r] - mean;
+            sq += d * d;
+        }
+    sq += __shfl_xor(sq, 32);
+    const float rstd = 1.0f / sqrtf(sq / (float)kRows + eps);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float v = (y[t][r] - mean) * rstd * gamma[hid(t, r, 0)] + beta[hid(t, r, 0)];
+            y[t][r] = v < 0.0f ? 0.0f : v;  // ReLU (NaN passes, as torch.relu)
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one tile's parameters in registers at a time
+    }
+}
+
+struct FwdArgs {
+    const float* obs;
+    float* out;
+    uint8_t* actions;
+    float* log_prob;
+    uint64_t seed;
+    int64_t step;
+    int64_t env_id_base;
+    int64_t n;
+};
+
+// -log p(y | logit) of torch's binary_cross_entropy_with_logits, as
+// Bernoulli.log_prob evaluates it (probs clamped to [eps, 1 - eps] first).
+__device__ __forceinline__ float bernoulli_nll(float p, float y) {
+    const float pc = fminf(fmaxf(p, FLT_EPSILON), 1.0f - FLT_EPSILON);
+    const float x = logf(pc) - log1pf(-pc);
+    const float m = fmaxf(-x, 0.0f);
+    return (1.0f - y) * x + m + logf(expf(-m) + expf(-x - m));
+}
+
+template <int K>
+__global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__ packed, FwdArgs p) {
+    extern __shared__ f32x4 lds4[];
+    const float* lds = reinterpret_cast<const float*>(lds4);
+    for (int i = threadIdx.x; i < kPacked / 4; i += kThreads) lds4[i] = reinterpret_cast<const f32x4*>(packed)[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+    const float eps = lds[kB4 + 3];
+    const int64_t tiles = (p.n + kCols - 1) / kCols;
+    for (int64_t tile = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); tile < tiles;
+         tile += (int64_t)gridDim.x * kWaves) {
+        const int64_t d = tile * kCols + c;  // this lane's drone (column)
+        const bool live = d < p.n;
+        float x[kSteps1];  // B operands of layer 1: obs[d][2q + h]
+#pragma unroll
+        for (int q = 0; q < kSteps1; ++q) {
+            const int k = 2 * q + h;
+            x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
+        }
+
+        f32x16 acc4[4];
+        float y1[4][16], y2[4][16];
+        layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4);
+        bias_norm_relu<4>(acc4, lds + kV1, eps, h, y1);
+        layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4);
+        bias_norm_relu<4>(acc4, lds + kV2, eps, h, y2);
+        f32x16 acc2[2];
+        float y3[2][16];
+        layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2);
+        bias_norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        __builtin_amdgcn_sched_barrier(0);
+
+        float z[K];  // Linear(64, K): 32 rows per lane half, then the other half's
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float* w = lds + kW4 + k * 64 + 4 * h;
+            float s = 0.0f;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s += w[hid(t, r, 0)] * y3[t][r];
+            s += __shfl_xor(s, 32);
+            z[k] = s + lds[kB4 + k];
+        }
+        if (!live || h != 0) continue;
+        if constexpr (K == 1) {
+            if (p.out) p.out[d] = z[0];
+        } else {
+            float prob[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) prob[k] = 1.0f / (1.0f + expf(-z[k]));  // Sigmoid
+            if (p.out) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) p.out[d * K + k] = prob[k];
+            }
+            if (p.actions || p.log_prob) {
+                const uint64_t env = (uint64_t)(p.env_id_base + d), st = (uint64_t)p.step;
+                uint32_t r[4];
+                philox4x32_10((uint32_t)env, (uint32_t)(env >> 32), (uint32_t)st, (uint32_t)(st >> 32) ^ 0x5A5A5A5Au,
+                              (uint32_t)p.seed, (uint32_t)(p.seed >> 32), r);
+                uint32_t bits = 0;
+                float lp = 0.0f;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const float u = (float)(r[k] >> 8) * 0x1p-24f;  // uniform [0, 1), 24 bits
+                    const bool on = u < prob[k];
+                    bits |= on ? (1u << k) : 0u;
+                    lp -= bernoulli_nll(prob[k], on ? 1.0f : 0.0f);
+                }
+                if (p.actions) p.actions[d] = (uint8_t)bits;
+                if (p.log_prob) p.log_prob[d] = lp;
+            }
+        }
+    }
+}
+
+template <int K>
+hipError_t launch(const float* packed, const FwdArgs& a, hipStream_t s) {
+    static bool configured = false;  // the LDS image exceeds the 64 KB default
+    if (!configured) {
+        const hipError_t e = hipFuncSetAttribute((const void*)mlp_kernel<K>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+        if (e != hipSuccess) return e;
+        configured = true;
+    }
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const int64_t tiles = (a.n + kCols - 1) / kCols;
+    const int64_t want = (tiles + kWaves - 1) / kWaves;
+    const unsigned blocks = (unsigned)(want < cus ? want : cus);  // one block per CU, waves loop over tiles
+    hipLaunchKernelGGL(mlp_kernel<K>, dim3(blocks), dim3(kThreads), kLdsBytes, s, packed, a);
+    return hipGetLastError();
+}
+
+}  // namespace mlp
+}  // namespace dd
+
+extern "C" {
+
+int64_t dd_mlp_packed_floats(void) { return dd::mlp::kPacked; }
+
+int dd_mlp_pack(const DDMlpParams* p, float* packed, void* stream) {
+    if (!p || !packed || !(p->out_dim == 1 || p->out_dim == 3) || !(p->ln_eps > 0.0f)) return hipErrorInvalidValue;
+    const float* req[] = {p->w0, p->b0, p->ln1_w, p->ln1_b, p->w3, p->b3, p->ln4_w,
+                          p->ln4_b, p->w6, p->b6, p->ln7_w, p->ln7_b, p->w9, p->b9};
+    for (const float* q : req)
+        if (!q) return hipErrorInvalidValue;
+    const int threads = 256, blocks = (dd::mlp::kPacked + threads - 1) / threads;
+    hipLaunchKernelGGL(dd::mlp::pack_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, *p, packed);
+    return hipGetLastError();
+}
+
+int dd_mlp_forward(const float* packed, int32_t out_dim, const DDMlpIO* io, int64_t n, void* stream) {
+    if (!io || n < 0 || !(out_dim == 1 || out_dim == 3)) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    if (!packed || !io->obs) return hipErrorInvalidValue;
+    if (out_dim == 1 && (io->actions || io->log_prob)) return hipErrorInvalidValue;  // nothing to sample
+    const dd::mlp::FwdArgs a{io->obs, io->out, io->actions, io->log_prob, io->seed, io->step, io->env_id_base, n};
+    return out_dim == 3 ? dd::mlp::launch<3>(packed, a, (hipStream_t)stream)
+                        : dd::mlp::launch<1>(packed, a, (hipStream_t)stream);
+}
+
+}  // extern "C"

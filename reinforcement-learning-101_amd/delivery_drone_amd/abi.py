@@ -15,11 +15,11 @@ import torch  # noqa: F401  -- must be loaded first so the library binds torch's
 __all__ = [
     "DD_F32", "DD_F64", "DD_ACT_BITMASK", "DD_ACT_F32X3", "DD_ACT_U8X3", "DD_ACT_PHILOX",
     "DD_ST_DONE", "DD_ST_LANDED", "DD_ST_CRASHED", "DD_ST_PLAT_LEFT", "DD_OBS_DIM",
-    "DDConfig", "DDState", "DDStepIO", "DDRolloutIO", "lib", "load", "library_path", "check",
+    "DDConfig", "DDState", "DDStepIO", "DDRolloutIO", "DDMlpParams", "DDMlpIO", "lib", "load", "library_path", "check",
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 2
+DD_ABI_VERSION = 3
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
@@ -88,6 +88,20 @@ class DDRolloutIO(ctypes.Structure):
     ]
 
 
+class DDMlpParams(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in (
+        "w0", "b0", "ln1_w", "ln1_b", "w3", "b3", "ln4_w", "ln4_b",
+        "w6", "b6", "ln7_w", "ln7_b", "w9", "b9")] + [("out_dim", _I), ("ln_eps", ctypes.c_float)]
+
+
+class DDMlpIO(ctypes.Structure):
+    _fields_ = [
+        ("obs", ctypes.c_void_p), ("out", ctypes.c_void_p), ("actions", ctypes.c_void_p),
+        ("log_prob", ctypes.c_void_p), ("seed", ctypes.c_uint64), ("step", ctypes.c_int64),
+        ("env_id_base", ctypes.c_int64),
+    ]
+
+
 #: every symbol include/dronestep.h declares, with its ctypes signature
 EXPORTS = {
     "dd_config_default": (None, [ctypes.POINTER(DDConfig)]),
@@ -108,6 +122,10 @@ EXPORTS = {
     "dd_compact_workspace": (ctypes.c_int64, [ctypes.c_int64]),
     "dd_compact": (ctypes.c_int, [ctypes.c_void_p, _I, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "dd_mlp_packed_floats": (ctypes.c_int64, []),
+    "dd_mlp_pack": (ctypes.c_int, [ctypes.POINTER(DDMlpParams), ctypes.c_void_p, ctypes.c_void_p]),
+    "dd_mlp_forward": (ctypes.c_int, [ctypes.c_void_p, _I, ctypes.POINTER(DDMlpIO), ctypes.c_int64,
+                                      ctypes.c_void_p]),
     "dd_step_bytes_per_env": (ctypes.c_int64, [_I, _I, _I]),
     "dd_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dd_abi_version": (ctypes.c_int, []),

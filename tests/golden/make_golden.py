@@ -10,7 +10,8 @@ engine's attributes to the fixture inputs and records what ``step()`` /
 reference source is copied.  The GPU box never runs this script: it only
 reads the .npz / .json files written here.
 
-    python -B tests/golden/make_golden.py
+    python -B tests/golden/make_golden.py                  # every fixture
+    python -B tests/golden/make_golden.py --only policy    # policy.npz alone
 """
 from __future__ import annotations
 
@@ -455,7 +456,65 @@ def gae_set(seed=5, T=257, cols=48, gamma=0.99, lam=0.95) -> dict:
                 gamma=np.float64(gamma), lam=np.float64(lam))
 
 
+# The notebooks' policy / value networks
+def policy_set(seed=11, games=24, frames=120) -> dict:
+    """DroneGamerBoi / DroneTeacherBoi of Actor_Critic_PPO.ipynb:376-424,
+    executed from the notebook's cells, with the trained weights of
+    models/actor-critic-ppo/*.pth (state_dicts, loaded weights_only=True).
+    Inputs are observations of reference games under random actions plus
+    synthetic rows; outputs are the notebook models' float32 CPU results and
+    Bernoulli.log_prob of fixed action draws (:857-859).  The weights are
+    stored as plain float arrays so the GPU box can rebuild the networks."""
+    import json as _json
+    import torch
+    from torch import nn
+    from torch.distributions import Bernoulli
+    nb = _json.load(open(os.path.join(REF, "Actor_Critic_PPO.ipynb")))
+    ns = {"torch": torch, "nn": nn, "np": np, "device": torch.device("cpu"), "DroneState": type("DroneState", (), {})}
+    for cell in nb["cells"]:
+        src = "".join(cell["source"])
+        if cell["cell_type"] == "code" and ("class DroneGamerBoi" in src or "class DroneTeacherBoi" in src):
+            exec(compile(src, "Actor_Critic_PPO.ipynb", "exec"), ns)
+    actor, critic = ns["DroneGamerBoi"](), ns["DroneTeacherBoi"]()
+    mdir = os.path.join(REF, "models", "actor-critic-ppo")
+    actor.load_state_dict(torch.load(os.path.join(mdir, "drone_policy_v1.pth"), map_location="cpu",
+                                     weights_only=True))
+    critic.load_state_dict(torch.load(os.path.join(mdir, "drone_critic_v1.pth"), map_location="cpu",
+                                      weights_only=True))
+    rng = np.random.default_rng(seed)
+    rows = []
+    for g in range(games):
+        game = new_game(randomize_drone=True, randomize_platform=True)
+        state = game.reset()
+        for _ in range(frames):
+            rows.append(obs_vec(state))
+            state, _, done, _ = game.step(act_dict(int(rng.integers(0, 8))))
+            if done:
+                rows.append(obs_vec(state))
+                state = game.reset()
+    obs = np.asarray(rows, dtype=np.float32)
+    synth = rng.normal(0, 1.5, (256, 15)).astype(np.float32)
+    synth[:, 13:] = (rng.random((256, 2)) < 0.1).astype(np.float32)
+    synth[0] = 0.0
+    obs = np.concatenate([obs, synth])
+    with torch.no_grad():
+        x = torch.from_numpy(obs)
+        probs = actor(x)
+        values = critic(x)
+    actions = (rng.random((obs.shape[0], 3)) < 0.5).astype(np.float32)
+    log_prob = Bernoulli(probs=probs).log_prob(torch.from_numpy(actions)).sum(dim=1)
+    out = dict(obs=obs, probs=probs.numpy(), values=values.numpy(), actions=actions, log_prob=log_prob.numpy())
+    for tag, net in (("actor", actor), ("critic", critic)):
+        for k, v in net.state_dict().items():
+            out[f"{tag}.{k}"] = v.numpy()
+    return out
+
+
 def main():
+    if sys.argv[1:] == ["--only", "policy"]:
+        np.savez_compressed(os.path.join(HERE, "policy.npz"), **policy_set())
+        print("policy fixture written to", HERE)
+        return
     rng = np.random.default_rng(20261015)
     kats = notebook_kats()
     with open(os.path.join(HERE, "kat_notebooks.json"), "w") as f:
@@ -484,6 +543,7 @@ def main():
                         **shaped_set(np.random.default_rng(777), {"broad": 1200, "pad": 1200, "ground": 400,
                                                                  "bounds": 200}))
     np.savez_compressed(os.path.join(HERE, "gae.npz"), **gae_set())
+    np.savez_compressed(os.path.join(HERE, "policy.npz"), **policy_set())
     print("fixtures written to", HERE)
 
 

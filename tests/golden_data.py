@@ -82,3 +82,28 @@ def f32_close(got, ref, ulps: float = 2.0, atol: float = 0.0) -> np.ndarray:
     got = np.asarray(got, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     return np.abs(got - ref) <= ulps * ulp32(ref) + atol
+
+
+def policy_fixture():
+    """policy.npz: obs, the notebook models' outputs, and both state_dicts
+    ({"actor": {...}, "critic": {...}}, keys without the 'network.' prefix)."""
+    d = npz("policy.npz")
+    nets = {tag: {k[len(tag) + len(".network."):]: v for k, v in d.items() if k.startswith(tag + ".network.")}
+            for tag in ("actor", "critic")}
+    return d, nets
+
+
+def torch_mlp(sd: dict, device="cpu"):
+    """The notebooks' network body (Actor_Critic_PPO.ipynb:376-424) as a plain
+    torch fp32 module loaded with `sd`: the floating-point reference the HIP
+    kernel is compared with.  Sigmoid is appended for the 3-output actor."""
+    import torch
+    from torch import nn
+    k = sd["9.weight"].shape[0]
+    layers = [nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128), nn.LayerNorm(128), nn.ReLU(),
+              nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(), nn.Linear(64, k)]
+    if k == 3:
+        layers.append(nn.Sigmoid())
+    net = nn.Sequential(*layers)
+    net.load_state_dict({kk: torch.as_tensor(v) for kk, v in sd.items()})
+    return net.to(device).eval()

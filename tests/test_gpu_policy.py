@@ -1,0 +1,148 @@
+"""GPU: dd_mlp_forward (the notebooks' actor / critic on f32 MFMA) against the
+notebook models' own outputs (tests/golden/policy.npz) and a torch fp32
+reference, plus the Bernoulli sampling contract.
+
+Tolerances (float32 model, different summation order than torch's):
+probabilities |d| <= 2e-6; values |d| <= 1e-5 * (1 + |v|) ... 2e-4 absolute at
+|v| ~ 600; log-probabilities |d| <= 1e-5 * (1 + |lp|)."""
+import numpy as np
+import pytest
+import torch
+from torch.distributions import Bernoulli
+
+import golden_data as gd
+from delivery_drone_amd import MlpNet, VecDroneEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def close(got, want, rel, abs_):
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    err = np.abs(got - want)
+    bound = abs_ + rel * np.abs(want)
+    assert np.all(err <= bound), f"max err {err.max():.3g} at {np.argmax(err - bound)}"
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    return gd.policy_fixture()
+
+
+def test_actor_probs_match_notebook_model(fixture, gpu_device):
+    d, nets = fixture
+    actor = MlpNet(nets["actor"], device=gpu_device)
+    probs = actor(torch.as_tensor(d["obs"], device=gpu_device))
+    close(probs.cpu().numpy(), d["probs"], 0.0, 2e-6)
+
+
+def test_critic_values_match_notebook_model(fixture, gpu_device):
+    d, nets = fixture
+    critic = MlpNet(nets["critic"], device=gpu_device)
+    assert critic.out_dim == 1
+    v = critic(torch.as_tensor(d["obs"], device=gpu_device))
+    close(v.cpu().numpy(), d["values"], 2e-6, 1e-4)
+
+
+def test_log_prob_of_sampled_actions(fixture, gpu_device):
+    d, nets = fixture
+    actor = MlpNet(nets["actor"], device=gpu_device)
+    obs = torch.as_tensor(d["obs"], device=gpu_device)
+    actions, lp, probs = actor.act(obs, seed=3, step=17, probs=True)
+    bits = torch.stack([(actions >> j) & 1 for j in range(3)], dim=1).float()
+    want = Bernoulli(probs=probs).log_prob(bits).sum(1)
+    close(lp.cpu().numpy(), want.cpu().numpy(), 1e-5, 1e-5)
+    # and against the notebook model's probabilities directly
+    want_nb = Bernoulli(probs=torch.as_tensor(d["probs"])).log_prob(bits.cpu()).sum(1)
+    close(lp.cpu().numpy(), want_nb.numpy(), 1e-5, 2e-5)
+
+
+def test_sampling_is_bernoulli(fixture, gpu_device):
+    """Bit j of the action is set with probability p_j: 64 draws (steps) of
+    every fixture row; z-scores of the per-bit totals."""
+    d, nets = fixture
+    actor = MlpNet(nets["actor"], device=gpu_device)
+    obs = torch.as_tensor(d["obs"], device=gpu_device)
+    p = actor(obs).double()
+    hits = torch.zeros_like(p)
+    draws = 64
+    for s in range(draws):
+        a, _ = actor.act(obs, seed=99, step=s)
+        hits += torch.stack([((a >> j) & 1).double() for j in range(3)], dim=1)
+    mean = (p * draws).sum(0)
+    var = (p * (1 - p) * draws).sum(0)
+    z = ((hits.sum(0) - mean) / var.sqrt()).cpu().numpy()
+    assert np.all(np.abs(z) < 5.0), z
+
+
+def test_samples_are_keyed_by_env_and_step(fixture, gpu_device):
+    d, nets = fixture
+    actor = MlpNet(nets["actor"], device=gpu_device)
+    obs = torch.as_tensor(d["obs"], device=gpu_device)
+    a, lp = actor.act(obs, seed=5, step=40)
+    a2, lp2 = actor.act(obs, seed=5, step=40)
+    assert torch.equal(a, a2) and torch.equal(lp, lp2)
+    cut = 1000  # two shards with their global env ids draw what the full batch draws
+    b0, _ = actor.act(obs[:cut], seed=5, step=40)
+    b1, _ = actor.act(obs[cut:], seed=5, step=40, env_id_base=cut)
+    assert torch.equal(torch.cat([b0, b1]), a)
+    a3, _ = actor.act(obs, seed=5, step=41)
+    assert not torch.equal(a, a3)
+
+
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 4097, 65_536 + 37])
+def test_random_weights_vs_torch_fp32(n, gpu_device):
+    """Freshly initialised networks (torch's default init) at ragged and
+    config-5 sizes against torch on the same device."""
+    torch.manual_seed(n)
+    for k in (3, 1):
+        sd = _random_sd(k)
+        ref = gd.torch_mlp({kk: v.numpy() for kk, v in sd.items()}, device=gpu_device)
+        net = MlpNet(sd, device=gpu_device)
+        obs = torch.randn(n, 15, device=gpu_device) * 2.0
+        with torch.no_grad():
+            want = ref(obs)
+        got = net(obs)
+        if k == 1:
+            want = want[:, 0]
+        close(got.cpu().numpy(), want.cpu().numpy(), 1e-4 if k == 1 else 0.0, 1e-5 if k == 3 else 1e-4)
+
+
+def _random_sd(k):
+    from torch import nn
+    layers = [nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128), nn.LayerNorm(128), nn.ReLU(),
+              nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(), nn.Linear(64, k)]
+    net = nn.Sequential(*layers)
+    with torch.no_grad():  # non-trivial LayerNorm affine parameters
+        for i in (1, 4, 7):
+            net[i].weight.uniform_(0.5, 1.5)
+            net[i].bias.uniform_(-0.2, 0.2)
+    return net.state_dict()
+
+
+def test_policy_driven_rollout_matches_host_loop(fixture, gpu_device):
+    """obs -> dd_mlp_forward (sample) -> dd_step for 40 frames, all on the
+    device, equals the same loop with actions copied through the host."""
+    d, nets = fixture
+    actor = MlpNet(nets["actor"], device=gpu_device)
+    a_env = VecDroneEnv(2048, device=gpu_device, randomize_drone=True, auto_reset=True, seed=4)
+    b_env = VecDroneEnv(2048, device=gpu_device, randomize_drone=True, auto_reset=True, seed=4)
+    oa, ob = a_env.reset(), b_env.reset()
+    for t in range(40):
+        acts, _ = actor.act(oa, seed=8, step=t)
+        oa, ra, da, _ = a_env.step(acts)
+        host = actor.act(ob, seed=8, step=t)[0].cpu()
+        ob, rb, db, _ = b_env.step(host.to(gpu_device))
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
+
+
+def test_errors(fixture, gpu_device):
+    d, nets = fixture
+    critic = MlpNet(nets["critic"], device=gpu_device)
+    with pytest.raises(ValueError):
+        critic.act(torch.zeros(4, 15, device=gpu_device))
+    with pytest.raises(ValueError):
+        critic(torch.zeros(4, 14, device=gpu_device))
+    bad = dict(nets["actor"])
+    bad["3.weight"] = bad["3.weight"][:, :64]
+    with pytest.raises(ValueError):
+        MlpNet(bad, device=gpu_device)
