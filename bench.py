@@ -242,6 +242,91 @@ def notebook_point(n, precision, seed, dev):
             "kernel": "dd::step_kernel<float, 0, true, true> (reward_mode='notebook')"}
 
 
+MLP_FLOPS_PER_ROW = 2 * (15 * 128 + 128 * 128 + 128 * 64 + 64 * 3)  # the notebooks' actor, algorithmic
+F32_MFMA_PEAK_TFS = 157.3  # MI355X dense f32 MFMA (MI355X_MICROARCH.md, Matrix cores)
+
+
+def _random_actor(dev, seed):
+    """The notebooks' DroneGamerBoi body with torch's default init (random
+    weights of that architecture; no checkpoint travels to the box)."""
+    import torch
+    from torch import nn
+    from delivery_drone_amd import MlpNet
+    torch.manual_seed(seed)
+    net = nn.Sequential(nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128), nn.LayerNorm(128),
+                        nn.ReLU(), nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(), nn.Linear(64, 3))
+    return MlpNet(net.state_dict(), device=dev)
+
+
+def policy_point(n, seed, dev):
+    """the actor forward + Bernoulli sample + log-prob
+    (dd_mlp_forward) over n observation rows; bound = f32 MFMA."""
+    import torch
+    actor = _random_actor(dev, seed)
+    obs = torch.randn(n, 15, device=dev)
+    acts = torch.empty(n, dtype=torch.uint8, device=dev)
+    lp = torch.empty(n, device=dev)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        actor.act(obs, actions_out=acts, log_prob_out=lp)
+        torch.cuda.synchronize(dev)
+        reps = 50
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for s in range(reps):
+            actor.act(obs, step=s, actions_out=acts, log_prob_out=lp)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    tfs = n * MLP_FLOPS_PER_ROW / (us * 1e-6) / 1e12
+    del actor, obs, acts, lp
+    torch.cuda.empty_cache()
+    return {"rows": n, "us": round(us, 2), "rows_per_s": round(n / (us * 1e-6), 1),
+            "roofline": {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_row": MLP_FLOPS_PER_ROW},
+            "kernel": "dd::mlp::mlp_kernel<3> (dd_mlp_forward: actor + Bernoulli sample + log-prob, f32 MFMA)"}
+
+
+def policy_rollout_point(n, frames, seed, dev):
+    """Policy in the loop, nothing on the host: per frame dd_mlp_forward
+    (sample from the current obs) then dd_step, `frames` frames captured in
+    one hipGraph.  env-steps/s with the actor's inference included."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv
+    actor = _random_actor(dev, seed)
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg)
+    obs = env.reset()
+    acts = torch.empty(n, dtype=torch.uint8, device=dev)
+    lp = torch.empty(n, device=dev)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        for t in range(3):
+            actor.act(obs, step=t, actions_out=acts, log_prob_out=lp)
+            env.step(acts)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for t in range(frames):
+                actor.act(env.obs, step=t, actions_out=acts, log_prob_out=lp)
+                env.step(acts)
+        g.replay()
+        torch.cuda.synchronize(dev)
+        reps = 5
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del actor, env, acts, lp, g
+    torch.cuda.empty_cache()
+    return {"envs": n, "frames": frames, "ms": round(ms, 3), "steps_per_s": round(n * frames / (ms * 1e-3), 1),
+            "us_per_frame": round(ms * 1e3 / frames, 2),
+            "launch": f"hipGraph of {frames} x (dd_mlp_forward + dd_step)"}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -344,12 +429,14 @@ def main():
     hbm = None
     if world == 1 and args.hbm_point > 0:
         hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
-    c5 = g5 = nb = None
+    c5 = g5 = nb = pp = pr = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         g5 = gae_point(args.rollout_point, 256, dev)
     if world == 1 and args.extra_points:
         nb = notebook_point(n, args.precision, args.seed, dev)
+        pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
+        pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
 
     if rank == 0:
         total_steps = n * world * args.steps
@@ -400,6 +487,8 @@ def main():
             "rollout_point": c5,
             "gae_point": g5,
             "notebook_reward_point": nb,
+            "policy_point": pp,
+            "policy_rollout_point": pr,
             "gpu_ms_per_step": round(step_ms, 6),
             "device": torch.cuda.get_device_name(dev),
         }

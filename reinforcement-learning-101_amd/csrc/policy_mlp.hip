@@ -39,9 +39,13 @@ namespace mlp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kIn = DD_OBS_DIM;  // 15
-constexpr int kWaves = 8;
+#ifndef DD_MLP_WAVES
+#define DD_MLP_WAVES 8  // per block (one block per CU); experiments try 4 / 12
+#endif
+constexpr int kWaves = DD_MLP_WAVES;
 constexpr int kThreads = kWaves * 64;
 constexpr int kCols = 32;  // drones per wave tile
 
@@ -105,12 +109,16 @@ __global__ void pack_kernel(DDMlpParams p, float* out) {
     out[i] = v;
 }
 
-// out^T tiles (NT of 32 rows) += W . in^T over STEPS k-steps; bval(q) is the
-// lane's B operand (its column's input at the k of step q).
+// out^T tiles (NT of 32 rows) = bias + W . in^T over STEPS k-steps; bval(q)
+// is the lane's B operand (its column's input at the k of step q); bias_h =
+// the layer's bias + 4h (this lane half's rows).
 template <int NT, int STEPS, typename BVal>
-__device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lane, BVal bval, f32x16 (&acc)[NT]) {
+__device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lane, BVal bval, f32x16 (&acc)[NT],
+                                           const float* bias_h) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    for (int t = 0; t < NT; ++t)  // the bias is the accumulator's initial value
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = bias_h[hid(t, r, 0)];
 #pragma unroll
     for (int g = 0; g < STEPS / 4; ++g) {
         f32x4 a[NT];
@@ -126,43 +134,49 @@ __device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lan
     }
 }
 
-// + bias, LayerNorm over the column's 32*NT rows (biased variance, as
-// nn.LayerNorm), ReLU.  vec = [bias | weight | bias] of 32*NT each.
+// LayerNorm over the column's 32*NT rows (biased variance, as nn.LayerNorm),
+// then ReLU.  vec = [Linear bias | LN weight | LN bias] of 32*NT each.  Pairs
+// of registers hold adjacent rows, so the arithmetic runs as packed f32
+// (v_pk_add / v_pk_fma), in torch's form y = (x * rstd - rstd * mean) *
+// weight + bias.
 template <int NT>
-__device__ __forceinline__ void bias_norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
-                                               float (&y)[NT][16]) {
+__device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
+                                          float (&y)[NT][16]) {
     constexpr int kRows = 32 * NT;
-    const float* bias = vec + 4 * h;
     const float* gamma = vec + kRows + 4 * h;
     const float* beta = vec + 2 * kRows + 4 * h;
-    float sum = 0.0f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            y[t][r] = acc[t][r] + bias[hid(t, r, 0)];
-            sum += y[t][r];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    sum += __shfl_xor(sum, 32);
-    const float mean = sum / (float)kRows;
-    float sq = 0.0f;
+    f32x2 s2 = {0.0f, 0.0f};
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float d = y[t][r] - mean;
-            sq += d * d;
+        for (int r = 0; r < 16; r += 2) s2 += f32x2{acc[t][r], acc[t][r + 1]};
+    float sum = s2.x + s2.y;
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum / (float)kRows;
+    const f32x2 m2 = {mean, mean};
+    f32x2 q2 = {0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const f32x2 d = f32x2{acc[t][r], acc[t][r + 1]} - m2;
+            q2 = __builtin_elementwise_fma(d, d, q2);
         }
+    float sq = q2.x + q2.y;
     sq += __shfl_xor(sq, 32);
     const float rstd = 1.0f / sqrtf(sq / (float)kRows + eps);
+    const f32x2 rs2 = {rstd, rstd}, nb2 = {-rstd * mean, -rstd * mean};
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float v = (y[t][r] - mean) * rstd * gamma[hid(t, r, 0)] + beta[hid(t, r, 0)];
-            y[t][r] = v < 0.0f ? 0.0f : v;  // ReLU (NaN passes, as torch.relu)
+        for (int r = 0; r < 16; r += 2) {
+            const int row = hid(t, r, 0);  // rows row, row + 1 (r even)
+            const f32x2 g = *reinterpret_cast<const f32x2*>(gamma + row);
+            const f32x2 b = *reinterpret_cast<const f32x2*>(beta + row);
+            const f32x2 xn = __builtin_elementwise_fma(f32x2{acc[t][r], acc[t][r + 1]}, rs2, nb2);
+            const f32x2 v = __builtin_elementwise_fma(xn, g, b);
+            y[t][r] = fmaxf(v.x, 0.0f);  // ReLU
+            y[t][r + 1] = fmaxf(v.y, 0.0f);
         }
         __builtin_amdgcn_sched_barrier(0);  // one tile's parameters in registers at a time
     }
@@ -179,13 +193,13 @@ struct FwdArgs {
     int64_t n;
 };
 
-// -log p(y | logit) of torch's binary_cross_entropy_with_logits, as
-// Bernoulli.log_prob evaluates it (probs clamped to [eps, 1 - eps] first).
-__device__ __forceinline__ float bernoulli_nll(float p, float y) {
+// log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
+// as torch's Bernoulli does (probs_to_logits, clamp_probs): log p or
+// log1p(-p).  (torch evaluates it as -BCE-with-logits of the logit; the two
+// agree to float32 rounding.)
+__device__ __forceinline__ float bernoulli_logp(float p, bool on) {
     const float pc = fminf(fmaxf(p, FLT_EPSILON), 1.0f - FLT_EPSILON);
-    const float x = logf(pc) - log1pf(-pc);
-    const float m = fmaxf(-x, 0.0f);
-    return (1.0f - y) * x + m + logf(expf(-m) + expf(-x - m));
+    return on ? logf(pc) : log1pf(-pc);
 }
 
 template <int K>
@@ -211,25 +225,28 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
 
         f32x16 acc4[4];
         float y1[4][16], y2[4][16];
-        layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4);
-        bias_norm_relu<4>(acc4, lds + kV1, eps, h, y1);
-        layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4);
-        bias_norm_relu<4>(acc4, lds + kV2, eps, h, y2);
+        layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
+        norm_relu<4>(acc4, lds + kV1, eps, h, y1);
+        layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4, lds + kV2 + 4 * h);
+        norm_relu<4>(acc4, lds + kV2, eps, h, y2);
         f32x16 acc2[2];
         float y3[2][16];
-        layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2);
-        bias_norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2, lds + kV3 + 4 * h);
+        norm_relu<2>(acc2, lds + kV3, eps, h, y3);
         __builtin_amdgcn_sched_barrier(0);
 
         float z[K];  // Linear(64, K): 32 rows per lane half, then the other half's
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const float* w = lds + kW4 + k * 64 + 4 * h;
-            float s = 0.0f;
+            f32x2 s2 = {0.0f, 0.0f};
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) s += w[hid(t, r, 0)] * y3[t][r];
+                for (int r = 0; r < 16; r += 2)
+                    s2 = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(w + hid(t, r, 0)),
+                                                   f32x2{y3[t][r], y3[t][r + 1]}, s2);
+            float s = s2.x + s2.y;
             s += __shfl_xor(s, 32);
             z[k] = s + lds[kB4 + k];
         }
@@ -256,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
                     const float u = (float)(r[k] >> 8) * 0x1p-24f;  // uniform [0, 1), 24 bits
                     const bool on = u < prob[k];
                     bits |= on ? (1u << k) : 0u;
-                    lp -= bernoulli_nll(prob[k], on ? 1.0f : 0.0f);
+                    lp += bernoulli_logp(prob[k], on);
                 }
                 if (p.actions) p.actions[d] = (uint8_t)bits;
                 if (p.log_prob) p.log_prob[d] = lp;

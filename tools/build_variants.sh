@@ -6,13 +6,17 @@ cd "$(dirname "$0")/../reinforcement-learning-101_amd"
 OUT=delivery_drone_amd/_native/lab
 mkdir -p $OUT
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I../include"
-build() { /opt/rocm/bin/hipcc $FLAGS "${@:2}" -o $OUT/lib_$1.so csrc/drone_step.hip & }
+build() { /opt/rocm/bin/hipcc $FLAGS "${@:2}" -o $OUT/lib_$1.so csrc/drone_step.hip csrc/policy_mlp.hip & }
 # "prev": the committed source at $PREV_REV (default HEAD), for before/after runs
 if [ -n "${PREV_REV:-HEAD}" ] && git -C .. rev-parse -q --verify "${PREV_REV:-HEAD}" > /dev/null 2>&1; then
   mkdir -p /tmp/dd_prev
   git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/drone_step.hip" > /tmp/dd_prev/drone_step.hip
-  git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/trig.h" > /tmp/dd_prev/trig.h 2>/dev/null || true
-  /opt/rocm/bin/hipcc $FLAGS -Icsrc -o $OUT/lib_prev.so /tmp/dd_prev/drone_step.hip &
+  PREV_SRCS=/tmp/dd_prev/drone_step.hip
+  for f in trig.h philox.h policy_mlp.hip; do
+    git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/$f" > /tmp/dd_prev/$f 2>/dev/null || rm -f /tmp/dd_prev/$f
+  done
+  [ -f /tmp/dd_prev/policy_mlp.hip ] && PREV_SRCS="$PREV_SRCS /tmp/dd_prev/policy_mlp.hip"
+  /opt/rocm/bin/hipcc $FLAGS -Icsrc -o $OUT/lib_prev.so $PREV_SRCS &
 fi
 for v in ${VARIANTS:-base}; do
   case $v in
@@ -23,6 +27,8 @@ for v in ${VARIANTS:-base}; do
     plainout) build plainout -DDD_PLAIN_OUT_STORES ;;
     nomath) build nomath -DDD_EXP_NOMATH ;;
     obsmul) build obsmul -DDD_OBS_MUL ;;
+    mlpw4) build mlpw4 -DDD_MLP_WAVES=4 ;;
+    mlpw12) build mlpw12 -DDD_MLP_WAVES=12 ;;
     empty) build empty -DDD_EXP_EMPTY ;;
     b512) build b512 -DDD_STEP_BLOCK=512 ;;
     b1024) build b1024 -DDD_STEP_BLOCK=1024 ;;
