@@ -327,6 +327,44 @@ def policy_rollout_point(n, frames, seed, dev):
             "launch": f"hipGraph of {frames} x (dd_mlp_forward + dd_step)"}
 
 
+def socket_point(seed, dev, steps=2000):
+    """STEP round trips through the JSON-lines socket
+    server (reference protocol) from one client on 127.0.0.1, like the
+    reference's benchmark_latency (socket_client.py:227-282)."""
+    import json as _json
+    import socket
+    from delivery_drone_amd import VecDroneEnv
+    from delivery_drone_amd.server import BatchSocketServer
+    env = VecDroneEnv(1, device=dev, auto_reset=False, randomize_drone=True, seed=seed, precision="f64")
+    env.reset()
+    srv = BatchSocketServer(env, "127.0.0.1", 0).start()
+    try:
+        sock = socket.create_connection(("127.0.0.1", srv.port), timeout=30)
+        sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        f = sock.makefile("rb")
+        f.readline()  # HANDSHAKE
+        step = (_json.dumps({"type": "STEP", "game_id": 0, "action": {"main_thrust": 1}}) + "\n").encode()
+        reset = (_json.dumps({"type": "RESET", "game_id": 0}) + "\n").encode()
+
+        def run(k):
+            for _ in range(k):
+                sock.sendall(step)
+                if _json.loads(f.readline())["done"]:
+                    sock.sendall(reset)
+                    f.readline()
+
+        run(50)
+        t0 = time.perf_counter()
+        run(steps)
+        dt = time.perf_counter() - t0
+        sock.close()
+    finally:
+        srv.stop()
+    return {"steps": steps, "steps_per_s": round(steps / dt, 1), "ms_per_step": round(dt * 1e3 / steps, 4),
+            "transport": "TCP 127.0.0.1, JSON lines, one client, sequential STEP requests",
+            "reference_published": "300-500 steps/s (delivery_drone/SOCKET_API.md:373)"}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -429,7 +467,7 @@ def main():
     hbm = None
     if world == 1 and args.hbm_point > 0:
         hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
-    c5 = g5 = nb = pp = pr = None
+    c5 = g5 = nb = pp = pr = sp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         g5 = gae_point(args.rollout_point, 256, dev)
@@ -437,6 +475,7 @@ def main():
         nb = notebook_point(n, args.precision, args.seed, dev)
         pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
         pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
+        sp = socket_point(args.seed, dev)
 
     if rank == 0:
         total_steps = n * world * args.steps
@@ -489,6 +528,7 @@ def main():
             "notebook_reward_point": nb,
             "policy_point": pp,
             "policy_rollout_point": pr,
+            "socket_point": sp,
             "gpu_ms_per_step": round(step_ms, 6),
             "device": torch.cuda.get_device_name(dev),
         }

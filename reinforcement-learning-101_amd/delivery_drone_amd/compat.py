@@ -15,11 +15,13 @@ are for compatibility.  Throughput code calls :class:`VecDroneEnv` directly.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
 import torch
 
+from . import abi
 from .vec_env import OBS_KEYS, VecDroneEnv
 
 __all__ = ["DroneState", "DroneGameClient", "DroneGame", "action_bits"]
@@ -64,46 +66,72 @@ def _state_dict(obs_row, steps: int) -> dict:
 
 
 class _Lanes:
-    """Host-side readback of single lanes of a VecDroneEnv."""
+    """Single-lane calls on a VecDroneEnv and their host readback: every
+    request costs its kernel(s) plus ONE device-to-host copy of the lane's
+    values (the reference returns Python objects per call)."""
 
     def __init__(self, env: VecDroneEnv):
         self.env = env
+        self._di = torch.empty(2, dtype=env.float_dtype, device=env.device)  # distance, speed of one lane
+
+    def _lane_kernels(self, g: int, obs: bool):
+        e = self.env
+        st = e._sub_state(g, 1)
+        if obs:
+            abi.check(e._lib.dd_write_obs(ctypes.byref(e._cfg), ctypes.byref(st), e.obs[g].data_ptr(), 1,
+                                          e._stream()), "dd_write_obs")
+        abi.check(e._lib.dd_get_info(ctypes.byref(e._cfg), ctypes.byref(st), self._di.data_ptr(),
+                                     self._di[1:].data_ptr(), 1, e._stream()), "dd_get_info")
+
+    def _read(self, g: int, extra: Optional[torch.Tensor] = None):
+        e = self.env
+        sl = slice(g, g + 1)
+        f64 = torch.float64
+        parts = [e.obs[g].to(f64), e.steps[sl].to(f64), e.total_reward[sl].to(f64), e.episode[sl].to(f64),
+                 e.fuel[sl].to(f64), self._di.to(f64), e.angle[sl].to(f64), e.reward[sl].to(f64),
+                 e.status[sl].to(f64)]
+        if extra is not None:
+            parts.append(extra.to(f64))
+        vals = torch.cat(parts).cpu().tolist()
+        self._extra = vals[24:]
+        steps = int(vals[15])
+        info = {"steps": steps, "total_reward": vals[16], "episode": int(vals[17]), "fuel_remaining": vals[18],
+                "distance_to_platform": vals[19], "speed": vals[20], "angle": vals[21]}
+        return _state_dict(vals[:15], steps), info, vals[22], int(vals[23])
 
     def obs_dict(self, g: int) -> dict:
-        e = self.env
-        row = e.obs[g].tolist()
-        return _state_dict(row, int(e.steps[g].item()))
+        self._lane_kernels(g, obs=False)
+        return self._read(g)[0]
 
     def info(self, g: int) -> dict:
-        e = self.env
-        info = e.get_info()
-        return {
-            "steps": int(e.steps[g].item()),
-            "total_reward": float(e.total_reward[g].item()),
-            "episode": int(e.episode[g].item()),
-            "fuel_remaining": float(e.fuel[g].item()),
-            "distance_to_platform": float(info["distance_to_platform"][g].item()),
-            "speed": float(info["speed"][g].item()),
-            "angle": float(e.angle[g].item()),
-        }
+        self._lane_kernels(g, obs=False)
+        return self._read(g)[1]
 
     def step(self, g: int, action: Dict) -> Tuple[dict, float, bool, dict]:
         e = self.env
-        was_done = bool(e.status[g].item() & 1)
         a = torch.tensor([action_bits(action)], dtype=torch.uint8, device=e.device)
+        was = e.status[g:g + 1].clone()  # the pre-step status, read back with the rest
         e.step(a, lanes=slice(g, g + 1))
-        info = self.info(g)
-        if was_done and not e.config.auto_reset:
+        self._lane_kernels(g, obs=False)
+        state, info, reward, status = self._read(g, was)
+        if int(self._extra[0]) & 1 and not e.config.auto_reset:
             info["needs_reset"] = True  # game_engine.py:107-111
-        return self.obs_dict(g), float(e.reward[g].item()), bool(e.done[g].item()), info
+        return state, reward, bool(status & 1), info
 
     def reset(self, g: int) -> dict:
         self.env.reset(lanes=slice(g, g + 1))
-        return self.obs_dict(g)
+        self._lane_kernels(g, obs=False)
+        return self._read(g)[0]
 
     def get_state(self, g: int) -> dict:
-        self.env.get_state()
-        return self.obs_dict(g)
+        self._lane_kernels(g, obs=True)
+        return self._read(g)[0]
+
+    def get_state_info(self, g: int):
+        """(state, done, info) of GET_STATE (socket_server.py:211-214), one readback."""
+        self._lane_kernels(g, obs=True)
+        state, info, _, status = self._read(g)
+        return state, bool(status & 1), info
 
 
 class DroneGameClient:
