@@ -171,8 +171,11 @@ __device__ __forceinline__ void measure(Lane& s) {
 
 // DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
 // Platform.reset (platform.py:104-114).  `c` is the call's config (switches,
-// spawn ranges, seed); s.episode becomes the value after `episode += 1`.
-__device__ __forceinline__ void spawn(const DDConfig& c, int64_t env, Lane& s) {
+// spawn ranges, seed), `max_fuel` the physics' (compile-time under kRef, so
+// a rollout's frame loop issues no scalar load that a join's lgkmcnt wait
+// would couple to its LDS reads); s.episode becomes the value after
+// `episode += 1`.
+__device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_t env, Lane& s) {
     s.episode += 1;
     uint32_t r[4];
     philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)s.episode, 0u,
@@ -192,7 +195,7 @@ __device__ __forceinline__ void spawn(const DDConfig& c, int64_t env, Lane& s) {
         s.py = c.platform_start_y;
     }
     s.vx = 0.0; s.vy = 0.0; s.angle = 0.0; s.omega = 0.0;
-    s.fuel = c.max_fuel;
+    s.fuel = max_fuel;
     s.status = 0u;  // not done / landed / crashed; platform direction +1
     s.steps = 0;
     s.total = 0.0;
@@ -550,7 +553,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
         reward = 0.0;
         if (sw.auto_reset) {  // next-step reset: fresh episode, reward 0, done 0
             s.episode = at(a.episode, i);
-            spawn(sw, a.env_id_base + i, s);
+            spawn(sw, k.c.max_fuel, a.env_id_base + i, s);
             respawned = true;
             if constexpr (kShaped) {  // the notebook's history restarts: prev_state None
                 at(p.shaped_hist, i) = trig::div_exact(s.dist, k.c.world_width, k.inv_w);
@@ -690,9 +693,73 @@ __device__ __forceinline__ void quantize(Lane& s) {
     s.omega = (T)s.omega; s.fuel = (T)s.fuel; s.px = (T)s.px; s.py = (T)s.py; s.total = (T)s.total;
 }
 
-template <typename T, int AFMT, bool kRef>
+// A kernel's by-value Soa argument (placed after `Args` in the kernarg
+// segment) read again through an opaque pointer.  The frame loop of
+// rollout_kernel does not touch the state arrays, but with `a` itself used
+// after the loop the compiler kept its 26 pointer SGPRs live across the loop
+// and spilled them to VGPR lanes; the second read lets them die.
+template <typename Args, typename T>
+__device__ __forceinline__ Soa<T> reload_soa() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr size_t off = (sizeof(Args) + alignof(Soa<T>) - 1) / alignof(Soa<T>) * alignof(Soa<T>);
+    uint64_t kp = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    typedef const __attribute__((address_space(4))) Soa<T> KSoa;
+    const KSoa* q = reinterpret_cast<KSoa*>(kp + off);
+    Soa<T> r;
+    r.x = q->x; r.y = q->y; r.vx = q->vx; r.vy = q->vy; r.angle = q->angle; r.omega = q->omega;
+    r.fuel = q->fuel; r.px = q->px; r.py = q->py; r.total = q->total;
+    r.status = q->status; r.steps = q->steps; r.episode = q->episode; r.env_id_base = q->env_id_base;
+    return r;
+#else
+    return Soa<T>{};  // the host pass never runs device code
+#endif
+}
+
+// Rollout observation staging.  kHeld (every frame row of the launch starts
+// 16-byte aligned: obs aligned and N % 4 == 0, the usual case): two LDS
+// slices per wave; frame f's rows go into slice f & 1 while frame f - 1's
+// rows are read back into registers before frame f's arithmetic and stored
+// after it, so the LDS round trip and the stores overlap the frame instead
+// of following it (the rollout runs one wave per SIMD at 65,536 drones:
+// nothing else hides latency).  Every frame issues the same stores (4
+// predicated 16-byte stores + 1 predicated tail dword per lane), so the
+// vmcnt waits the compiler places for the action prefetch stay short.
+// !kHeld: one slice per wave, flushed after each frame.
+struct HeldObs {
+    f32x4 v[4];  // a 64-row slice is 240 float4: 3.75 per lane
+    float tail;  // rows * 15 % 4 floats past the last whole float4 (ragged wave)
+};
+
+// Reads the whole 64-row slice at wtile (plus padding: the tile carries
+// kHeldPad floats past its last slice), unconditionally so the four reads
+// issue back to back; store_held_wave writes only the nf = rows * 15 floats
+// that are rows.
+constexpr int kHeldPad = 4 * kWave * 4 - kWave * DD_OBS_DIM;  // 256 float4 read vs 240 in a slice
+
+__device__ __forceinline__ void hold_obs_wave(const float* wtile, int nf, HeldObs& h) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const f32x4* src4 = reinterpret_cast<const f32x4*>(wtile);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h.v[j] = src4[lane + j * kWave];
+    h.tail = wtile[((nf >> 2) << 2) + (lane & 3)];
+}
+
+__device__ __forceinline__ void store_held_wave(const HeldObs& h, float* dst, int nf) {
+    const int lane = threadIdx.x & (kWave - 1);
+    f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
+    const int nv = nf >> 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = lane + j * kWave;
+        if (k < nv) __builtin_nontemporal_store(h.v[j], &dst4[k]);
+    }
+    if (lane < (nf & 3)) __builtin_nontemporal_store(h.tail, dst + (nv << 2) + lane);
+}
+
+template <typename T, int AFMT, bool kRef, bool kHeld>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a) {
-    __shared__ __attribute__((aligned(16))) float tile[kBlock * DD_OBS_DIM];
+    __shared__ __attribute__((aligned(16))) float tile[kHeld ? 2 : 1][kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0)];
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     const uint32_t row0 = blockIdx.x * kBlock;
@@ -700,38 +767,77 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
     const bool live = i < (uint32_t)p.n;
     const uint32_t wrow0 = row0 + (threadIdx.x & ~(kWave - 1));  // this wave's first row
     const int wrows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
-    const float* wtile = tile + (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM;
-    float* orow = tile + threadIdx.x * DD_OBS_DIM;
+    const int wfloats = wrows * DD_OBS_DIM;
+    const int woff = (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM;  // the wave's slice in a tile
+    const int roff = threadIdx.x * DD_OBS_DIM;                   // the lane's row in a tile
     const int64_t env = a.env_id_base + i;
+    HeldObs held;
     Lane s;
-    uint32_t next = 0;
+    // Actions are prefetched two frames ahead into two registers used in
+    // turn (the loop is unrolled by two, so no register copy of a pending
+    // load): the load a frame consumes was issued before two frames' stores,
+    // and its vmcnt wait is long met.
+    uint32_t act0 = 0, act1 = 0;
     if (live) {
         load_dynamics(a, i, s);
         s.total = at(a.total, i);
         s.status = at(a.status, i);
         s.steps = at(a.steps, i);
         s.episode = at(a.episode, i);
-        next = rollout_action<AFMT>(p, env, 0, i);
     }
-    for (int f = 0; f < p.frames; ++f) {
-        const uint32_t act = next;
+    if (p.frames > 0) act0 = rollout_action<AFMT>(p, env, 0, live ? i : (uint32_t)p.n - 1);
+    if (p.frames > 1) act1 = rollout_action<AFMT>(p, env, 1, live ? i : (uint32_t)p.n - 1);
+    // every prologue load lands here, not at a wait inside the frame loop
+    asm volatile("" ::"v"(s.x), "v"(s.y), "v"(s.vx), "v"(s.vy), "v"(s.angle), "v"(s.omega), "v"(s.fuel),
+                 "v"(s.px), "v"(s.py), "v"(s.total), "v"(s.status), "v"(s.steps), "v"(s.episode), "v"(act0),
+                 "v"(act1));
+    auto run_frame = [&](const int f, uint32_t& slot) __attribute__((always_inline)) {
+        if (kHeld && p.obs && f > 0) {
+            __syncwarp();  // frame f - 1's rows (other lanes of this wave) are in LDS
+            hold_obs_wave(tile[(f - 1) & 1] + woff, wfloats, held);
+        }
+        // unconditional, for every lane (the last two frames re-read the last
+        // row, lanes past n read lane n - 1): a conditional load would leave
+        // a register copy of it, and that copy waits for the load
+#ifdef DD_EXP_ROLL_NOACT  // timing-only: actions from arithmetic, no loads
+        const uint32_t act = ((uint32_t)f * 2654435761u ^ i) >> 5 & 7u;
+        (void)slot;
+#else
+        const uint32_t act = slot;
+        slot = rollout_action<AFMT>(p, env, min(f + 2, p.frames - 1), live ? i : (uint32_t)p.n - 1);
+#endif
         if (live) {
-            if (f + 1 < p.frames) next = rollout_action<AFMT>(p, env, f + 1, i);
             double reward = 0.0;
             if (s.status & DD_ST_DONE) {
-                if (sw.auto_reset) spawn(sw, env, s);  // next-step reset
-                else measure(s);                       // sticky done
+                if (sw.auto_reset) spawn(sw, k.c.max_fuel, env, s);  // next-step reset
+                else measure(s);                                     // sticky done
             } else {
                 reward = frame(k, sw, act, s);
             }
             put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
             put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-            if (p.obs) observe(k, s, orow);
+            if (p.obs) observe(k, s, tile[kHeld ? (f & 1) : 0] + roff);
             quantize<T>(s);  // the obs above sees the unrounded frame, like dd_step's
         }
-        if (p.obs) flush_obs_wave(wtile, p.obs + ((size_t)f * p.n_total + wrow0) * DD_OBS_DIM, wrows);
+        if (p.obs) {
+            if constexpr (kHeld) {
+                if (f > 0) store_held_wave(held, p.obs + ((size_t)(f - 1) * p.n_total + wrow0) * DD_OBS_DIM, wfloats);
+            } else {
+                flush_obs_wave(tile[0] + woff, p.obs + ((size_t)f * p.n_total + wrow0) * DD_OBS_DIM, wrows);
+            }
+        }
+    };
+    for (int f = 0; f < p.frames; f += 2) {
+        run_frame(f, act0);
+        if (f + 1 < p.frames) run_frame(f + 1, act1);
     }
-    if (live) store_spawn(a, i, s);  // every field: lanes may have re-spawned
+    if (kHeld && p.obs && p.frames > 0) {  // the last frame's slice
+        const int f = p.frames - 1;
+        __syncwarp();
+        hold_obs_wave(tile[f & 1] + woff, wfloats, held);
+        store_held_wave(held, p.obs + ((size_t)f * p.n_total + wrow0) * DD_OBS_DIM, wfloats);
+    }
+    if (live) store_spawn(reload_soa<RolloutArgs, T>(), i, s);  // every field: lanes may have re-spawned
 }
 
 // dd_shaped_reset kernel: the notebook reward's history restarts from the
@@ -758,7 +864,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Consts k, Soa<T> a, const
     if (mask && !at(mask, i)) return;
     Lane s;
     s.episode = at(a.episode, i);
-    spawn(k.c, a.env_id_base + i, s);
+    spawn(k.c, k.c.max_fuel, a.env_id_base + i, s);
     store_spawn(a, i, s);
     if (obs) observe(k, s, obs + (size_t)i * DD_OBS_DIM);
 }
@@ -970,7 +1076,10 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
 
 template <typename T, int AFMT, bool kRef>
 void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
-    hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
+    // the held obs path needs every frame row start 16-byte aligned
+    const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0;
+    if (held) hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
+    else hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
 }
 
 template <typename T, bool kRef>

@@ -35,6 +35,7 @@ for v in ${VARIANTS:-base}; do
     b128) build b128 -DDD_STEP_BLOCK=128 ;;
     w8) build w8 -DDD_STEP_MIN_WAVES=8 ;;
     w4) build w4 -DDD_STEP_MIN_WAVES=4 ;;
+    rnoact) build rnoact -DDD_EXP_ROLL_NOACT ;;
     *) echo "unknown variant $v" >&2; exit 1 ;;
   esac
 done

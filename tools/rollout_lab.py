@@ -20,6 +20,7 @@ def main():
     p.add_argument("--envs", default="65536,262144")
     p.add_argument("--frames", type=int, default=256)
     p.add_argument("--rounds", type=int, default=7)
+    p.add_argument("--no-obs", action="store_true")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     cfg = EnvConfig(randomize_drone=True, auto_reset=True, seed=0)
@@ -32,20 +33,21 @@ def main():
         for v in args.variants.split(","):
             e = VecDroneEnv(n, device=dev, config=cfg, library=abi.load(os.path.join(LAB, f"lib_{v}.so")))
             e.reset()
-            e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)
+            e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done, write_obs=not args.no_obs)
             envs[v] = (e, [])
         torch.cuda.synchronize()
         for _ in range(args.rounds):
             for v, (e, ts) in envs.items():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)
+                e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done, write_obs=not args.no_obs)
                 e1.record()
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1))
         for v, (e, ts) in envs.items():
             med = statistics.median(ts)
-            print(json.dumps({"envs": n, "frames": args.frames, "variant": v, "ms_median": round(med, 4),
+            print(json.dumps({"envs": n, "frames": args.frames, "variant": v, "obs": not args.no_obs,
+                              "ms_median": round(med, 4),
                               "steps_per_s": round(n * args.frames / (med * 1e-3), 1)}), flush=True)
 
 
