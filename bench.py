@@ -193,6 +193,112 @@ def rollout_point(n, frames, precision, seed, dev):
     return out
 
 
+def step_loop_point(n, frames, precision, seed, dev):
+    """BASELINE config 5 variant (a): the same rollout as one dd_step launch
+    per frame (actions from a [frames, n] tensor, obs/reward/done written
+    straight into the rollout buffers with step(out=...)), the frames
+    captured in one hipGraph.  Per frame the state makes a full HBM round
+    trip, so bytes per env-frame are the step's 147 (f32, with obs)."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg, precision=precision)
+    env.reset()
+    acts = torch.randint(0, 8, (frames, n), device=dev, dtype=torch.uint8)
+    obs = torch.empty(frames, n, 15, device=dev)
+    rew = torch.empty(frames, n, device=dev, dtype=env.float_dtype)
+    done = torch.empty(frames, n, device=dev, dtype=torch.bool)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        for t in range(3):
+            env.step(acts[t], out=(obs[t], rew[t], done[t]))
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for t in range(frames):
+                env.step(acts[t], out=(obs[t], rew[t], done[t]))
+        g.replay()
+        torch.cuda.synchronize(dev)
+        reps = 5
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    bpe = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=True)
+    gbs = bpe * n * frames / (ms * 1e-3) / 1e9
+    del env, acts, obs, rew, done, g
+    torch.cuda.empty_cache()
+    return {"envs": n, "frames": frames, "ms_per_rollout": round(ms, 4),
+            "steps_per_s": round(n * frames / (ms * 1e-3), 1), "us_per_frame": round(ms * 1e3 / frames, 3),
+            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env_frame": bpe,
+            "launch": f"hipGraph of {frames} dd_step launches into [T, N] buffers"}
+
+
+def config2_point(seed, dev, n=4096):
+    """BASELINE config 2: 4096 drones, fixed spawn (drone 400,100; pad
+    400,500), f32 storage, auto-reset.  Launch-bound: one dd_step per frame
+    from a hipGraph, and the same frames as 256-frame dd_rollout launches."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv
+    cfg = EnvConfig(randomize_drone=False, randomize_platform=False, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg)
+    env.reset()
+    rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
+    ms = time_steps(env, rows, 2000, 100, torch.cuda.Stream(dev))
+    frames = 256
+    acts = torch.randint(0, 8, (frames, n), device=dev, dtype=torch.uint8)
+    obs = torch.empty(frames, n, 15, device=dev)
+    rew = torch.empty(frames, n, device=dev)
+    done = torch.empty(frames, n, device=dev, dtype=torch.bool)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)
+        torch.cuda.synchronize(dev)
+        reps = 20
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    rms = e0.elapsed_time(e1) / reps
+    del env, rows, acts, obs, rew, done
+    torch.cuda.empty_cache()
+    return {"envs": n, "spawn": "fixed", "us_per_step": round(ms * 1e3, 3),
+            "steps_per_s": round(n / (ms * 1e-3), 1), "launch": "hipGraph of 100 dd_step",
+            "rollout_ms_per_256_frames": round(rms, 4),
+            "rollout_steps_per_s": round(n * frames / (rms * 1e-3), 1)}
+
+
+def gather_point(env, n, world, backend, reps=5):
+    """BASELINE config 4's optional exchange: every rank's obs block [n, 15]
+    gathered to rank 0 (sharding.gather_obs: RCCL gather over xGMI), timed
+    outside the step loop.  Collective: every rank calls it."""
+    import torch
+    import torch.distributed as dist
+    from delivery_drone_amd.sharding import gather_obs
+    obs = env.obs if backend == "nccl" else env.obs.cpu()
+    gather_obs(obs, n * world)  # warm-up (communicator set-up)
+    torch.cuda.synchronize(env.device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = gather_obs(obs, n * world)
+    torch.cuda.synchronize(env.device)
+    dt = (time.perf_counter() - t0) / reps
+    t = torch.tensor([dt], dtype=torch.float64, device=env.device if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t[0])
+    nbytes = n * world * 15 * 4
+    del out
+    return {"rows": n * world, "bytes_to_rank0": nbytes, "ms": round(dt * 1e3, 3),
+            "GB_per_s": round(nbytes / dt / 1e9, 2), "backend": backend,
+            "note": "timed outside the step loop; the step path has no collective"}
+
+
 def gae_point(n, frames, dev):
     """dd_gae over a [frames, n] rollout: reads reward,
     value (+ bootstrap row), done; writes advantage and return."""
@@ -467,11 +573,16 @@ def main():
     hbm = None
     if world == 1 and args.hbm_point > 0:
         hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
-    c5 = g5 = nb = pp = pr = sp = None
+    gp = None
+    if world > 1:
+        gp = gather_point(env, n, world, args.dist_backend)
+    c5 = c5a = g5 = c2 = nb = pp = pr = sp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
+        c5a = step_loop_point(args.rollout_point, 256, args.precision, args.seed, dev)
         g5 = gae_point(args.rollout_point, 256, dev)
     if world == 1 and args.extra_points:
+        c2 = config2_point(args.seed, dev)
         nb = notebook_point(n, args.precision, args.seed, dev)
         pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
         pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
@@ -524,6 +635,9 @@ def main():
             "cpu_baseline": cpu,
             "hbm_point": hbm,
             "rollout_point": c5,
+            "step_loop_point": c5a,
+            "config2_point": c2,
+            "gather_point": gp,
             "gae_point": g5,
             "notebook_reward_point": nb,
             "policy_point": pp,

@@ -198,3 +198,22 @@ def test_rollout_switches(cfg, gpu_device):
         o, r, d, _ = loop.step(acts[t])
         assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
     assert_same_state(roll, loop)
+
+
+def test_step_out_buffers_equal_rollout(gpu_device):
+    """BASELINE config 5(a): one dd_step per frame writing straight into the
+    rollout buffers (step(out=...)) equals one dd_rollout launch."""
+    n, k = 4100, 30
+    roll, loop = twins(n, gpu_device, randomize_drone=True, auto_reset=True, seed=21)
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
+    obs, reward, done = roll.rollout(acts)
+    ob = torch.full((k, n, 15), float("nan"), device=gpu_device)
+    rw = torch.full((k, n), float("nan"), device=gpu_device)
+    dn = torch.zeros(k, n, dtype=torch.bool, device=gpu_device)
+    for t in range(k):
+        o, r, d, _ = loop.step(acts[t], out=(ob[t], rw[t], dn[t]))
+        assert o.data_ptr() == ob[t].data_ptr() and r.data_ptr() == rw[t].data_ptr()
+    assert torch.equal(ob, obs) and torch.equal(rw, reward) and torch.equal(dn, done)
+    assert_same_state(roll, loop)
+    with pytest.raises(ValueError):
+        loop.step(acts[0], out=(ob[0, :10], rw[0], dn[0]))
