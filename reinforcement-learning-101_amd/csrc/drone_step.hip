@@ -132,8 +132,11 @@ constexpr Consts make_consts(const DDConfig& c) {
 // spills).  Switches, spawn ranges, wind and seed always come from the call.
 __device__ constexpr Consts kRefConsts = make_consts(reference_config());
 
-// True when every double the frame reads (wind aside) equals config.py's.
+// True when every double the frame reads (wind aside) equals config.py's
+// and the run has neither wind nor a moving platform: the kernels' kRef
+// instantiation, whose frame compiles neither in.
 inline bool uses_reference_physics(const DDConfig& c) {
+    if (c.wind_enabled || c.platform_moving) return false;
     const DDConfig r = reference_config();
     const double* a = &c.gravity;
     const double* b = &r.gravity;
@@ -202,30 +205,69 @@ __device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_
     measure(s);
 }
 
+// physics.normalize_angle after one frame's turn.  |omega| stays near
+// 0.3 / (1 - 0.95) = 6 degrees per frame, so the angle leaves (-540, 540]
+// only if the caller wrote such an angle; then the loop form runs (a rare,
+// separate branch).  One exact +-360 equals the reference's while-loops
+// inside that range (NaN passes through both unchanged).
+__device__ __forceinline__ double wrap_angle(double a) {
+    double w = a > 180.0 ? a - 360.0 : a;
+    w = a < -180.0 ? a + 360.0 : w;
+    if (__builtin_expect(fabs(a) > 540.0, 0)) w = trig::normalize_angle(a);
+    return w;
+}
+
 // One frame of a live lane: Drone.apply_thrust (drone.py:44-76), wind
 // (game_engine.py:121-123), Drone.update (drone.py:78-103), Platform.update
 // (platform.py:31-49), _calculate_reward with _check_landing / _check_crash /
 // _check_out_of_bounds (game_engine.py:179-279).  `k` holds the physics
-// (compile-time in the reference instantiation), `sw` the call's switches.
-// Returns the reward.
+// (compile-time under kRef), `sw` the call's switches; kRef also means no
+// wind and a static platform (their code is not compiled in).  Returns the
+// reward.
+//
+// kFlat (the rollout kernel, one wave per SIMD at its usual size): the
+// common path is one basic block.  The thrusters are applied through
+// selects (the thrust vector's sincos runs for every lane; a wave almost
+// always has a lane firing its main engine anyway) and the angle wrap is a
+// select with a rare fallback, so the scheduler can interleave the frame's
+// independent chains (sincos, fuel and spin, the two square roots) where
+// no other wave fills the stalls: 65,536 x 256 frames 0.424 -> 0.403 ms.
+// The step kernel (four waves per SIMD) keeps the branches: selects cost it
+// VALU slots the other waves would use.  Only the bottom-centre test near
+// the pad (rare) branches in both.
+template <bool kRef, bool kFlat>
 __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
     const DDConfig& c = k.c;
-    const bool main_on = act & 1u, left_on = act & 2u, right_on = act & 4u;
 
-    if (main_on && s.fuel > 0.0) {
-        // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
+    // apply_thrust: each thruster gated on fuel > 0 at that moment, in order
+    const double ty = -c.main_thrust_power;
+    if constexpr (kFlat) {
+        const bool main_on = (act & 1u) && s.fuel > 0.0;
         double sa, ca;
-        sincos_deg(s.angle, &sa, &ca);
-        const double ty = -c.main_thrust_power;
-        s.vx += 0.0 * ca - ty * sa;
-        s.vy += 0.0 * sa + ty * ca;
-        s.fuel -= c.fuel_main;
+        sincos_deg(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
+        s.vx = main_on ? s.vx + (0.0 * ca - ty * sa) : s.vx;
+        s.vy = main_on ? s.vy + (0.0 * sa + ty * ca) : s.vy;
+        s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
+        const bool left_on = (act & 2u) && s.fuel > 0.0;
+        s.omega = left_on ? s.omega - c.side_thrust_power : s.omega;
+        s.fuel = left_on ? s.fuel - c.fuel_side : s.fuel;
+        const bool right_on = (act & 4u) && s.fuel > 0.0;
+        s.omega = right_on ? s.omega + c.side_thrust_power : s.omega;
+        s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
+    } else {
+        if ((act & 1u) && s.fuel > 0.0) {
+            double sa, ca;
+            sincos_deg(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)
+            s.vx += 0.0 * ca - ty * sa;
+            s.vy += 0.0 * sa + ty * ca;
+            s.fuel -= c.fuel_main;
+        }
+        if ((act & 2u) && s.fuel > 0.0) { s.omega -= c.side_thrust_power; s.fuel -= c.fuel_side; }
+        if ((act & 4u) && s.fuel > 0.0) { s.omega += c.side_thrust_power; s.fuel -= c.fuel_side; }
     }
-    if (left_on && s.fuel > 0.0) { s.omega -= c.side_thrust_power; s.fuel -= c.fuel_side; }
-    if (right_on && s.fuel > 0.0) { s.omega += c.side_thrust_power; s.fuel -= c.fuel_side; }
     s.fuel = s.fuel > 0.0 ? s.fuel : 0.0;  // max(0, fuel)
 
-    if (sw.wind_enabled) { s.vx += sw.wind_x; s.vy += sw.wind_y; }
+    if (!kRef && sw.wind_enabled) { s.vx += sw.wind_x; s.vy += sw.wind_y; }
 
     s.vy += c.gravity * c.dt;
     s.vx *= c.drag;
@@ -234,9 +276,9 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     s.y += s.vy * c.dt;
     s.angle += s.omega * c.dt;
     s.omega *= c.angular_drag;
-    s.angle = trig::normalize_angle(s.angle);
+    s.angle = kFlat ? wrap_angle(s.angle) : trig::normalize_angle(s.angle);
 
-    if (sw.platform_moving) {
+    if (!kRef && sw.platform_moving) {
         const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
         s.px += c.platform_speed * dir * c.dt;
         if (s.px <= c.platform_min_x) { s.px = c.platform_min_x; s.status &= ~DD_ST_PLAT_LEFT; }
@@ -292,13 +334,14 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
 // DroneGame.get_state (game_engine.py:140-177) in state_to_array order, as the
 // reference's doubles (columns 0-12; 13/14 are the landed / crashed flags);
 // measure() has run on `s`.
+template <bool kGuard = false>
 __device__ __forceinline__ void observe_values(const Consts& k, const Lane& s, double v[13]) {
     const DDConfig& c = k.c;
     const double dx = s.px - s.x, dy = s.py - s.y;
 #ifdef DD_OBS_MUL  // experiment: x * RN(1/d), one op per column instead of three
 #define DD_Q(x, d, inv) ((x) * (inv))
 #else
-#define DD_Q(x, d, inv) trig::div_exact((x), (d), (inv))
+#define DD_Q(x, d, inv) (kGuard ? trig::div_exact_guarded((x), (d), (inv)) : trig::div_exact((x), (d), (inv)))
 #endif
     v[0] = DD_Q(s.x, c.world_width, k.inv_w);
     v[1] = DD_Q(s.y, c.world_height, k.inv_h);
@@ -323,9 +366,10 @@ __device__ __forceinline__ void write_obs_row(const double v[13], uint32_t statu
     o[14] = (status & DD_ST_CRASHED) ? 1.0f : 0.0f;
 }
 
+template <bool kGuard = false>
 __device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o) {
     double v[13];
-    observe_values(k, s, v);
+    observe_values<kGuard>(k, s, v);
     write_obs_row(v, s.status, o);
 }
 
@@ -570,7 +614,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
         reward = s.x;
         s.status |= (s.y > 550.0) ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
 #else
-        reward = frame(k, sw, r.act, s);
+        reward = frame<kRef, false>(k, sw, r.act, s);
 #endif
         if constexpr (kShaped) {
             double v[13];
@@ -600,8 +644,9 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
         store_dynamics(a, j, s);
         at(a.steps, j) = s.steps;
         at(a.total, j) = (T)s.total;
-        if (sw.platform_moving || respawned) at(a.px, j) = (T)s.px;
-        if (sw.platform_moving || ended || respawned) at(a.status, j) = (uint8_t)s.status;
+        const bool moving = !kRef && sw.platform_moving;
+        if (moving || respawned) at(a.px, j) = (T)s.px;
+        if (moving || ended || respawned) at(a.status, j) = (uint8_t)s.status;
         if (respawned) { at(a.py, j) = (T)s.py; at(a.episode, j) = s.episode; }
     }
     put_out(static_cast<T*>(p.reward), i, (T)reward);
@@ -625,6 +670,20 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
     __shared__ __attribute__((aligned(16))) float tile[kStepBlock * DD_OBS_DIM];
     const uint32_t row0 = blockIdx.x * kStepBlock;
     const uint32_t i = row0 + threadIdx.x;
+#ifdef DD_EXP_STAGGER  // timing-only: later dispatch rounds start their loads later
+    {
+        const uint32_t round = blockIdx.x / (gridDim.x / 4 > 0 ? gridDim.x / 4 : 1);
+        for (uint32_t k = 0; k < round; ++k) __builtin_amdgcn_s_sleep(DD_EXP_STAGGER);
+    }
+#endif
+#ifdef DD_EXP_STAGGER2  // timing-only: the second half of the grid starts later
+    if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_sleep(DD_EXP_STAGGER2);
+#endif
+    // The load bases are wanted in SGPRs before the lane test: left to
+    // itself the compiler sank their kernarg loads into the `i < n` branch,
+    // one scalar-load latency later than the state loads could start.
+    asm volatile("" ::"s"(a.x), "s"(a.y), "s"(a.vx), "s"(a.vy), "s"(a.angle), "s"(a.omega), "s"(a.fuel),
+                 "s"(a.px), "s"(a.py), "s"(a.total), "s"(a.status), "s"(a.steps), "s"(p.actions));
     Raw<T> r;
     if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r);
     const bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM);
@@ -762,11 +821,19 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
     __shared__ __attribute__((aligned(16))) float tile[kHeld ? 2 : 1][kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0)];
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
+#ifdef DD_EXP_HALFWAVE  // timing-only: 32 drones per wave (lanes 32-63 idle), twice the waves
+    const uint32_t gwave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const uint32_t wrow0 = gwave * 32;
+    const uint32_t i = wrow0 + (threadIdx.x & (kWave - 1));
+    const bool live = (threadIdx.x & 32) == 0 && i < (uint32_t)p.n;
+    const int wrows = (int)min((int64_t)32, max((int64_t)0, (int64_t)p.n - wrow0));
+#else
     const uint32_t row0 = blockIdx.x * kBlock;
     const uint32_t i = row0 + threadIdx.x;
     const bool live = i < (uint32_t)p.n;
     const uint32_t wrow0 = row0 + (threadIdx.x & ~(kWave - 1));  // this wave's first row
     const int wrows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
+#endif
     const int wfloats = wrows * DD_OBS_DIM;
     const int woff = (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM;  // the wave's slice in a tile
     const int roff = threadIdx.x * DD_OBS_DIM;                   // the lane's row in a tile
@@ -812,11 +879,11 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
                 if (sw.auto_reset) spawn(sw, k.c.max_fuel, env, s);  // next-step reset
                 else measure(s);                                     // sticky done
             } else {
-                reward = frame(k, sw, act, s);
+                reward = frame<kRef, true>(k, sw, act, s);
             }
             put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
             put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-            if (p.obs) observe(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+            if (p.obs) observe<!kRef && std::is_same<T, double>::value>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
             quantize<T>(s);  // the obs above sees the unrounded frame, like dd_step's
         }
         if (p.obs) {
@@ -1078,8 +1145,13 @@ template <typename T, int AFMT, bool kRef>
 void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
     // the held obs path needs every frame row start 16-byte aligned
     const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0;
-    if (held) hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
-    else hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false>), dim3((unsigned)tiles_of(p.n)), dim3(kBlock), 0, s, p, a);
+#ifdef DD_EXP_HALFWAVE
+    const unsigned blocks = (unsigned)tiles_of(2 * (int64_t)p.n);
+#else
+    const unsigned blocks = (unsigned)tiles_of(p.n);
+#endif
+    if (held) hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true>), dim3(blocks), dim3(kBlock), 0, s, p, a);
+    else hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false>), dim3(blocks), dim3(kBlock), 0, s, p, a);
 }
 
 template <typename T, bool kRef>

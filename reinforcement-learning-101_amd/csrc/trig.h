@@ -102,6 +102,21 @@ DD_HD inline double div_exact(double x, double d, double inv_d) {
     return fma(r, inv_d, q0);
 }
 
+// div_exact with x passed through an empty asm between its two uses.  In the
+// kRef = false rollout kernels with f64 storage (d and inv_d in registers)
+// ROCm 7.2 wrote q0 over x's register and then read that register back as x
+// (v_fma_f64 D, -A, B, A: the quotient of the quotient).  The LLVM IR is
+// right; the guard changes the machine code's shape.  It costs registers,
+// so only those kernels use it; tools/scan_isa.py checks every build.
+DD_HD inline double div_exact_guarded(double x, double d, double inv_d) {
+    const double q0 = x * inv_d;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(x));
+#endif
+    const double r = fma(-q0, d, x);
+    return fma(r, inv_d, q0);
+}
+
 // physics.normalize_angle (physics.py:26-39) in O(1).  The reference's loops
 // subtract (add) 360 while the angle is > 180 (< -180).  For |a| < 2^55 each
 // a - 360 is exact (360 is a multiple of ulp(a)), so k passes of the loop

@@ -150,8 +150,13 @@ def test_notebook_kats(gpu_device):
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
-def test_vs_oracle_same_precision(precision, gpu_device):
-    """Broad random states: GPU vs the C oracle with the same storage width."""
+@pytest.mark.parametrize("extra", [{}, {"gravity": 0.31, "drag": 0.985, "main_thrust_power": 0.65},
+                                   {"platform_moving": True}, {"wind_enabled": True, "wind_x": 0.04, "wind_y": -0.01}],
+                         ids=["reference", "custom-physics", "moving", "wind"])
+def test_vs_oracle_same_precision(precision, extra, gpu_device):
+    """Broad random states: GPU vs the C oracle with the same storage width,
+    on the compile-time-constant kernels (reference physics) and the ones that
+    take the physics from the call (custom constants, wind, moving pad)."""
     rng = np.random.default_rng(3)
     n = 100_003  # ragged: not a multiple of the 256-lane tile
     rec = gd.npz("single_step.npz")
@@ -162,7 +167,7 @@ def test_vs_oracle_same_precision(precision, gpu_device):
     dt = np.float64 if precision == "f64" else np.float32
     st = {k: (v.astype(dt) if v.dtype == np.float64 else v) for k, v in st.items()}
     acts = rng.integers(0, 8, n).astype(np.uint8)
-    cfg = EnvConfig(auto_reset=True, randomize_drone=True, seed=9)
+    cfg = EnvConfig(auto_reset=True, randomize_drone=True, seed=9, **extra)
     env = VecDroneEnv(n, precision=precision, device=gpu_device, config=cfg)
     oenv = ora.OracleEnv(n, precision=precision, config=cfg)
     load(env, st)

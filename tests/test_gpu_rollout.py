@@ -187,12 +187,16 @@ def test_rollout_large_ragged_equals_step_loop(gpu_device):
     assert_same_state(roll, loop)
 
 
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("n", [777, 4100])
 @pytest.mark.parametrize("cfg", [dict(platform_moving=True), dict(wind_enabled=True, wind_x=0.05, wind_y=-0.02),
-                                 dict(auto_reset=False)])
-def test_rollout_switches(cfg, gpu_device):
-    """dd_rollout with the moving platform, wind and sticky done (f64 storage)."""
-    roll, loop = twins(777, gpu_device, "f64", randomize_drone=True, seed=14, **cfg)
-    acts = torch.randint(0, 8, (80, 777), device=gpu_device, dtype=torch.uint8)
+                                 dict(auto_reset=False), dict(gravity=0.31, auto_reset=True)])
+def test_rollout_switches(cfg, n, precision, gpu_device):
+    """dd_rollout with the moving platform, wind, sticky done and non-reference
+    physics: the kernels without compile-time constants (where ROCm 7.2 once
+    miscompiled the f64 observation, tools/scan_isa.py), both obs paths."""
+    roll, loop = twins(n, gpu_device, precision, randomize_drone=True, seed=14, **cfg)
+    acts = torch.randint(0, 8, (80, n), device=gpu_device, dtype=torch.uint8)
     obs, reward, done = roll.rollout(acts)
     for t in range(80):
         o, r, d, _ = loop.step(acts[t])

@@ -57,8 +57,10 @@ def main():
                 g.replay()
             torch.cuda.synchronize(dev)
             runs[name] = (env, g, [])
-        for _ in range(args.rounds):
-            for name, (env, g, times) in runs.items():
+        names = list(runs)
+        for rnd in range(args.rounds):  # ABBA: alternate the order so position effects cancel
+            for name in (names if rnd % 2 == 0 else names[::-1]):
+                env, g, times = runs[name]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 with torch.cuda.stream(stream):
                     e0.record(stream)

@@ -36,8 +36,10 @@ def main():
             e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done, write_obs=not args.no_obs)
             envs[v] = (e, [])
         torch.cuda.synchronize()
-        for _ in range(args.rounds):
-            for v, (e, ts) in envs.items():
+        names = list(envs)
+        for rnd in range(args.rounds):  # ABBA: alternate the order so position effects cancel
+            for v in (names if rnd % 2 == 0 else names[::-1]):
+                e, ts = envs[v]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done, write_obs=not args.no_obs)
