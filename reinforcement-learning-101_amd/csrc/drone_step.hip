@@ -729,6 +729,18 @@ struct RolloutArgs {
     int64_t action_step;
 };
 
+// A wave-uniform pointer the compiler cannot prove uniform (it comes from
+// threadIdx-derived arithmetic, or is hoisted into a VGPR), moved to SGPRs so
+// loads and stores use the SGPR-base + 32-bit lane offset form and its
+// arithmetic stays on the scalar unit.
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* q) {
+    const uint64_t v = reinterpret_cast<uint64_t>(q);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<P*>(((uint64_t)hi << 32) | lo);
+}
+
 template <int AFMT>
 __device__ __forceinline__ uint32_t rollout_action(const RolloutArgs& p, int64_t env, int f, uint32_t i) {
     if constexpr (AFMT == DD_ACT_PHILOX) {
@@ -746,10 +758,13 @@ __device__ __forceinline__ uint32_t rollout_action(const RolloutArgs& p, int64_t
 
 // The state between two frames is what dd_step would store: rounded to the
 // storage width T (a no-op for double).
-template <typename T>
+// Under kRef the pad is static: px / py only change on a re-spawn, to
+// integers, which every storage width holds exactly.
+template <typename T, bool kRef = false>
 __device__ __forceinline__ void quantize(Lane& s) {
     s.x = (T)s.x; s.y = (T)s.y; s.vx = (T)s.vx; s.vy = (T)s.vy; s.angle = (T)s.angle;
-    s.omega = (T)s.omega; s.fuel = (T)s.fuel; s.px = (T)s.px; s.py = (T)s.py; s.total = (T)s.total;
+    s.omega = (T)s.omega; s.fuel = (T)s.fuel; s.total = (T)s.total;
+    if constexpr (!kRef) { s.px = (T)s.px; s.py = (T)s.py; }
 }
 
 // A kernel's by-value Soa argument (placed after `Args` in the kernarg
@@ -804,9 +819,17 @@ __device__ __forceinline__ void hold_obs_wave(const float* wtile, int nf, HeldOb
     h.tail = wtile[((nf >> 2) << 2) + (lane & 3)];
 }
 
+// dst is wave-uniform (SGPR base); a full slice (nf = 960: 240 float4) takes
+// three unpredicated stores and one for lanes < 48.
 __device__ __forceinline__ void store_held_wave(const HeldObs& h, float* dst, int nf) {
     const int lane = threadIdx.x & (kWave - 1);
-    f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
+    f32x4* dst4 = reinterpret_cast<f32x4*>(uniform_ptr(dst));
+    if (nf == kWave * DD_OBS_DIM) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) __builtin_nontemporal_store(h.v[j], &at(dst4, lane + j * kWave));
+        if (lane < kWave * DD_OBS_DIM / 4 - 3 * kWave) __builtin_nontemporal_store(h.v[3], &at(dst4, lane + 3 * kWave));
+        return;
+    }
     const int nv = nf >> 2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -816,77 +839,83 @@ __device__ __forceinline__ void store_held_wave(const HeldObs& h, float* dst, in
     if (lane < (nf & 3)) __builtin_nontemporal_store(h.tail, dst + (nv << 2) + lane);
 }
 
+#ifndef DD_ROLL_MIN_WAVES
+#define DD_ROLL_MIN_WAVES 1  // per SIMD; 4 caps the kernel at 128 VGPRs (A/B: DESIGN.md section 4)
+#endif
 template <typename T, int AFMT, bool kRef, bool kHeld>
-__global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a) {
+__global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(RolloutArgs p, Soa<T> a) {
     __shared__ __attribute__((aligned(16))) float tile[kHeld ? 2 : 1][kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0)];
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
-#ifdef DD_EXP_HALFWAVE  // timing-only: 32 drones per wave (lanes 32-63 idle), twice the waves
-    const uint32_t gwave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint32_t wrow0 = gwave * 32;
-    const uint32_t i = wrow0 + (threadIdx.x & (kWave - 1));
-    const bool live = (threadIdx.x & 32) == 0 && i < (uint32_t)p.n;
-    const int wrows = (int)min((int64_t)32, max((int64_t)0, (int64_t)p.n - wrow0));
-#else
     const uint32_t row0 = blockIdx.x * kBlock;
-    const uint32_t i = row0 + threadIdx.x;
-    const bool live = i < (uint32_t)p.n;
-    const uint32_t wrow0 = row0 + (threadIdx.x & ~(kWave - 1));  // this wave's first row
+    const bool live = row0 + threadIdx.x < (uint32_t)p.n;
+    // Lanes past n shadow lane n - 1: they load its state and action and
+    // compute its values, so its per-frame stores from them write the same
+    // bytes.  The frame loop then has no `live` branch (one basic block per
+    // frame on the common path); only the final state store is guarded.
+    const uint32_t i = live ? row0 + threadIdx.x : (uint32_t)p.n - 1;
+    // this wave's first row, its row count and slice offset: wave-uniform, in SGPRs
+    const uint32_t wrow0 = __builtin_amdgcn_readfirstlane(row0 + (threadIdx.x & ~(kWave - 1)));
     const int wrows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
-#endif
     const int wfloats = wrows * DD_OBS_DIM;
-    const int woff = (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM;  // the wave's slice in a tile
+    const int woff = (int)__builtin_amdgcn_readfirstlane((threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM);
     const int roff = threadIdx.x * DD_OBS_DIM;                   // the lane's row in a tile
     const int64_t env = a.env_id_base + i;
     HeldObs held;
     Lane s;
+    load_dynamics(a, i, s);
+    s.total = at(a.total, i);
+    s.status = at(a.status, i);
+    s.steps = at(a.steps, i);
+    s.episode = at(a.episode, i);
     // Actions are prefetched two frames ahead into two registers used in
     // turn (the loop is unrolled by two, so no register copy of a pending
     // load): the load a frame consumes was issued before two frames' stores,
     // and its vmcnt wait is long met.
     uint32_t act0 = 0, act1 = 0;
-    if (live) {
-        load_dynamics(a, i, s);
-        s.total = at(a.total, i);
-        s.status = at(a.status, i);
-        s.steps = at(a.steps, i);
-        s.episode = at(a.episode, i);
-    }
-    if (p.frames > 0) act0 = rollout_action<AFMT>(p, env, 0, live ? i : (uint32_t)p.n - 1);
-    if (p.frames > 1) act1 = rollout_action<AFMT>(p, env, 1, live ? i : (uint32_t)p.n - 1);
+    if (p.frames > 0) act0 = rollout_action<AFMT>(p, env, 0, i);
+    if (p.frames > 1) act1 = rollout_action<AFMT>(p, env, 1, i);
     // every prologue load lands here, not at a wait inside the frame loop
     asm volatile("" ::"v"(s.x), "v"(s.y), "v"(s.vx), "v"(s.vy), "v"(s.angle), "v"(s.omega), "v"(s.fuel),
                  "v"(s.px), "v"(s.py), "v"(s.total), "v"(s.status), "v"(s.steps), "v"(s.episode), "v"(act0),
                  "v"(act1));
-    auto run_frame = [&](const int f, uint32_t& slot) __attribute__((always_inline)) {
-        if (kHeld && p.obs && f > 0) {
+    // One frame; kObs and kAuto (auto_reset) are compile-time so the loop
+    // body carries no uniform branch on them.
+    auto run_frame = [&](const int f, uint32_t& slot, auto obs_c, auto auto_c) __attribute__((always_inline)) {
+        constexpr bool kObs = decltype(obs_c)::value, kAuto = decltype(auto_c)::value;
+        if (kHeld && kObs && f > 0) {
             __syncwarp();  // frame f - 1's rows (other lanes of this wave) are in LDS
             hold_obs_wave(tile[(f - 1) & 1] + woff, wfloats, held);
         }
-        // unconditional, for every lane (the last two frames re-read the last
-        // row, lanes past n read lane n - 1): a conditional load would leave
-        // a register copy of it, and that copy waits for the load
-#ifdef DD_EXP_ROLL_NOACT  // timing-only: actions from arithmetic, no loads
-        const uint32_t act = ((uint32_t)f * 2654435761u ^ i) >> 5 & 7u;
-        (void)slot;
-#else
+        // unconditional (the last two frames re-read the last row): a
+        // conditional load would leave a register copy of it, and that copy
+        // waits for the load
         const uint32_t act = slot;
-        slot = rollout_action<AFMT>(p, env, min(f + 2, p.frames - 1), live ? i : (uint32_t)p.n - 1);
-#endif
-        if (live) {
-            double reward = 0.0;
-            if (s.status & DD_ST_DONE) {
-                if (sw.auto_reset) spawn(sw, k.c.max_fuel, env, s);  // next-step reset
-                else measure(s);                                     // sticky done
-            } else {
-                reward = frame<kRef, true>(k, sw, act, s);
+        slot = rollout_action<AFMT>(p, env, min(f + 2, p.frames - 1), i);
+        double reward;
+        if constexpr (kAuto) {
+            // next-step reset, fixed up after the frame: every lane runs the
+            // frame (a done lane's result is discarded), and a wave with a lane
+            // to re-spawn takes the one branch
+            const bool was_done = (s.status & DD_ST_DONE) != 0;
+            reward = frame<kRef, true>(k, sw, act, s);
+            if (__ballot(was_done)) {
+                if (was_done) {
+                    spawn(sw, k.c.max_fuel, env, s);
+                    reward = 0.0;
+                }
             }
-            put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
-            put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-            if (p.obs) observe<!kRef && std::is_same<T, double>::value>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
-            quantize<T>(s);  // the obs above sees the unrounded frame, like dd_step's
+        } else if (s.status & DD_ST_DONE) {  // sticky done (game_engine.py:107-111)
+            measure(s);
+            reward = 0.0;
+        } else {
+            reward = frame<kRef, true>(k, sw, act, s);
         }
-        if (p.obs) {
+        put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
+        put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+        if constexpr (kObs) observe<!kRef && std::is_same<T, double>::value>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+        quantize<T, kRef>(s);  // the obs above sees the unrounded frame, like dd_step's
+        if constexpr (kObs) {
             if constexpr (kHeld) {
                 if (f > 0) store_held_wave(held, p.obs + ((size_t)(f - 1) * p.n_total + wrow0) * DD_OBS_DIM, wfloats);
             } else {
@@ -894,9 +923,20 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(RolloutArgs p, Soa<T> a
             }
         }
     };
-    for (int f = 0; f < p.frames; f += 2) {
-        run_frame(f, act0);
-        if (f + 1 < p.frames) run_frame(f + 1, act1);
+    auto run = [&](auto obs_c, auto auto_c) __attribute__((always_inline)) {
+        for (int f = 0; f < p.frames; f += 2) {
+            run_frame(f, act0, obs_c, auto_c);
+            if (f + 1 < p.frames) run_frame(f + 1, act1, obs_c, auto_c);
+        }
+    };
+    using yes = std::true_type;
+    using no = std::false_type;
+    if (p.obs) {
+        if (sw.auto_reset) run(yes{}, yes{});
+        else run(yes{}, no{});
+    } else {
+        if (sw.auto_reset) run(no{}, yes{});
+        else run(no{}, no{});
     }
     if (kHeld && p.obs && p.frames > 0) {  // the last frame's slice
         const int f = p.frames - 1;
@@ -1145,11 +1185,7 @@ template <typename T, int AFMT, bool kRef>
 void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
     // the held obs path needs every frame row start 16-byte aligned
     const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0;
-#ifdef DD_EXP_HALFWAVE
-    const unsigned blocks = (unsigned)tiles_of(2 * (int64_t)p.n);
-#else
     const unsigned blocks = (unsigned)tiles_of(p.n);
-#endif
     if (held) hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true>), dim3(blocks), dim3(kBlock), 0, s, p, a);
     else hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false>), dim3(blocks), dim3(kBlock), 0, s, p, a);
 }

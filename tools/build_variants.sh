@@ -35,14 +35,8 @@ for v in ${VARIANTS:-base}; do
     b128) build b128 -DDD_STEP_BLOCK=128 ;;
     w8) build w8 -DDD_STEP_MIN_WAVES=8 ;;
     w4) build w4 -DDD_STEP_MIN_WAVES=4 ;;
-    rnoact) build rnoact -DDD_EXP_ROLL_NOACT ;;
-    rhalf) build rhalf -DDD_EXP_HALFWAVE ;;
-    st8) build st8 -DDD_EXP_STAGGER=8 ;;
-    st16) build st16 -DDD_EXP_STAGGER=16 ;;
-    st32) build st32 -DDD_EXP_STAGGER=32 ;;
-    sh24) build sh24 -DDD_EXP_STAGGER2=24 ;;
-    sh48) build sh48 -DDD_EXP_STAGGER2=48 ;;
-    sh96) build sh96 -DDD_EXP_STAGGER2=96 ;;
+    rw2) build rw2 -DDD_ROLL_MIN_WAVES=2 ;;
+    rw4) build rw4 -DDD_ROLL_MIN_WAVES=4 ;;
     *) echo "unknown variant $v" >&2; exit 1 ;;
   esac
 done
