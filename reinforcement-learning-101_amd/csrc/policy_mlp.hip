@@ -134,6 +134,15 @@ __device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lan
     }
 }
 
+// x + (the same register of the other lane half), i.e. x + __shfl_xor(x, 32),
+// as one v_permlane32_swap (gfx950) instead of an LDS permute.  Lanes < 32
+// get x_l + x_{l+32}, lanes >= 32 x_{l-32} + x_l: the same sum (IEEE
+// addition is commutative).
+__device__ __forceinline__ float add_other_half(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // LayerNorm over the column's 32*NT rows (biased variance, as nn.LayerNorm),
 // then ReLU.  vec = [Linear bias | LN weight | LN bias] of 32*NT each.  Pairs
 // of registers hold adjacent rows, so the arithmetic runs as packed f32
@@ -150,8 +159,7 @@ __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* 
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) s2 += f32x2{acc[t][r], acc[t][r + 1]};
-    float sum = s2.x + s2.y;
-    sum += __shfl_xor(sum, 32);
+    const float sum = add_other_half(s2.x + s2.y);
     const float mean = sum / (float)kRows;
     const f32x2 m2 = {mean, mean};
     f32x2 q2 = {0.0f, 0.0f};
@@ -162,8 +170,7 @@ __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* 
             const f32x2 d = f32x2{acc[t][r], acc[t][r + 1]} - m2;
             q2 = __builtin_elementwise_fma(d, d, q2);
         }
-    float sq = q2.x + q2.y;
-    sq += __shfl_xor(sq, 32);
+    const float sq = add_other_half(q2.x + q2.y);
     const float rstd = 1.0f / sqrtf(sq / (float)kRows + eps);
     const f32x2 rs2 = {rstd, rstd}, nb2 = {-rstd * mean, -rstd * mean};
 #pragma unroll
@@ -246,9 +253,7 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
                 for (int r = 0; r < 16; r += 2)
                     s2 = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(w + hid(t, r, 0)),
                                                    f32x2{y3[t][r], y3[t][r + 1]}, s2);
-            float s = s2.x + s2.y;
-            s += __shfl_xor(s, 32);
-            z[k] = s + lds[kB4 + k];
+            z[k] = add_other_half(s2.x + s2.y) + lds[kB4 + k];
         }
         if (!live || h != 0) continue;
         if constexpr (K == 1) {

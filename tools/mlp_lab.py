@@ -44,8 +44,10 @@ def main():
             if err > 1e-5:
                 print(json.dumps({"variant": v, "rows": n, "MISMATCH": err}), flush=True)
         torch.cuda.synchronize()
-        for _ in range(args.rounds):
-            for v, (m, ts) in nets.items():
+        names = list(nets)
+        for rnd in range(args.rounds):  # ABBA: alternate the order so position effects cancel
+            for v in (names if rnd % 2 == 0 else names[::-1]):
+                m, ts = nets[v]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for s in range(args.reps):

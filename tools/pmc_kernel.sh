@@ -15,6 +15,7 @@ groups=(
  "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT"
  "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM"
 )
+[ -n "$EXTRA_GROUPS" ] && IFS=';' read -ra xg <<< "$EXTRA_GROUPS" && groups+=("${xg[@]}")
 LIBARG=""; [ -n "$LIB" ] && LIBARG="--lib $LIB"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace -f csv -- python3 tools/prof_driver.py --what $WHAT --envs $ENVS $LIBARG > /dev/null 2>> $OUT/err.log || { echo "trace failed"; exit 1; }
 i=0

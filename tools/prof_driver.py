@@ -33,6 +33,20 @@ def main():
         done = torch.empty(args.frames, n, device=dev, dtype=torch.bool)
         for _ in range(args.reps):
             env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)
+    elif args.what == "mlp":
+        from torch import nn
+        from delivery_drone_amd import MlpNet
+        torch.manual_seed(0)
+        net = nn.Sequential(nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128),
+                            nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(),
+                            nn.Linear(64, 3))
+        kw2 = {"library": lib} if lib is not None else {}
+        actor = MlpNet(net.state_dict(), device=dev, **kw2)
+        o = torch.randn(n, 15, device=dev)
+        acts_out = torch.empty(n, dtype=torch.uint8, device=dev)
+        lp = torch.empty(n, device=dev)
+        for k in range(args.reps):
+            actor.act(o, step=k, actions_out=acts_out, log_prob_out=lp)
     elif args.what == "step":
         rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
         for k in range(args.reps):
