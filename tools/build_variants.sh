@@ -29,10 +29,6 @@ for v in ${VARIANTS:-base}; do
     obsmul) build obsmul -DDD_OBS_MUL ;;
     mlpw4) build mlpw4 -DDD_MLP_WAVES=4 ;;
     mlpw12) build mlpw12 -DDD_MLP_WAVES=12 ;;
-    sk1) build sk1 -DDD_EXP_MLP_SKEW=1 ;;
-    sk2) build sk2 -DDD_EXP_MLP_SKEW=2 ;;
-    sk4) build sk4 -DDD_EXP_MLP_SKEW=4 ;;
-    sk8) build sk8 -DDD_EXP_MLP_SKEW=8 ;;
     empty) build empty -DDD_EXP_EMPTY ;;
     b512) build b512 -DDD_STEP_BLOCK=512 ;;
     b1024) build b1024 -DDD_STEP_BLOCK=1024 ;;
