@@ -670,15 +670,6 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
     __shared__ __attribute__((aligned(16))) float tile[kStepBlock * DD_OBS_DIM];
     const uint32_t row0 = blockIdx.x * kStepBlock;
     const uint32_t i = row0 + threadIdx.x;
-#ifdef DD_EXP_STAGGER  // timing-only: later dispatch rounds start their loads later
-    {
-        const uint32_t round = blockIdx.x / (gridDim.x / 4 > 0 ? gridDim.x / 4 : 1);
-        for (uint32_t k = 0; k < round; ++k) __builtin_amdgcn_s_sleep(DD_EXP_STAGGER);
-    }
-#endif
-#ifdef DD_EXP_STAGGER2  // timing-only: the second half of the grid starts later
-    if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_sleep(DD_EXP_STAGGER2);
-#endif
     // The load bases are wanted in SGPRs before the lane test: left to
     // itself the compiler sank their kernarg loads into the `i < n` branch,
     // one scalar-load latency later than the state loads could start.
