@@ -581,7 +581,10 @@ def main():
         hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
     gp = None
     if world > 1:
-        gp = gather_point(env, n, world, args.dist_backend)
+        try:  # an optional extra: a failure here must not cost the step measurement
+            gp = gather_point(env, n, world, args.dist_backend)
+        except Exception as e:  # noqa: BLE001
+            gp = {"error": f"{type(e).__name__}: {e}"[:300]}
     c5 = c5a = g5 = c2 = nb = pp = pr = sp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
