@@ -439,6 +439,40 @@ def policy_rollout_point(n, frames, seed, dev):
             "launch": f"hipGraph of {frames} x (dd_mlp_forward + dd_step)"}
 
 
+def render_point(seed, dev, frames=64, reps=20):
+    """DroneGame.render('rgb_array') as dd_render, `frames`
+    lanes of a running batch per launch (HUD and game-over overlay on).
+    Bound by the frame bytes it writes: 800 x 600 x 3 per frame."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv
+    env = VecDroneEnv(4096, device=dev, config=EnvConfig(randomize_drone=True, auto_reset=True, seed=seed))
+    env.reset()
+    acts = torch.randint(0, 8, (4096,), device=dev, dtype=torch.uint8)
+    for _ in range(40):
+        env.step(acts)
+    lanes = torch.arange(0, 4096, 4096 // frames, dtype=torch.int32, device=dev)[:frames]
+    out = torch.empty(frames, 600, 800, 3, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        env.render(lanes=lanes, out=out)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            env.render(lanes=lanes, out=out)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    nbytes = frames * 600 * 800 * 3
+    gbs = nbytes / (us * 1e-6) / 1e9
+    res = {"frames": frames, "us": round(us, 2), "frames_per_s": round(frames / (us * 1e-6), 1),
+           "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes": nbytes,
+           "kernel": "dd::render::render_kernel (dd_render, rgb_array 800x600, HUD on)"}
+    del env, out
+    torch.cuda.empty_cache()
+    return res
+
+
 def socket_point(seed, dev, steps=2000):
     """STEP round trips through the JSON-lines socket
     server (reference protocol) from one client on 127.0.0.1, like the
@@ -585,7 +619,7 @@ def main():
             gp = gather_point(env, n, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
             gp = {"error": f"{type(e).__name__}: {e}"[:300]}
-    c5 = c5a = g5 = c2 = nb = pp = pr = sp = None
+    c5 = c5a = g5 = c2 = nb = pp = pr = sp = rp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         c5a = step_loop_point(args.rollout_point, 256, args.precision, args.seed, dev)
@@ -596,6 +630,7 @@ def main():
         pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
         pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
         sp = socket_point(args.seed, dev)
+        rp = render_point(args.seed, dev)
 
     if rank == 0:
         total_steps = n * world * args.steps
@@ -652,6 +687,7 @@ def main():
             "policy_point": pp,
             "policy_rollout_point": pr,
             "socket_point": sp,
+            "render_point": rp,
             "gpu_ms_per_step": round(step_ms, 6),
             "device": torch.cuda.get_device_name(dev),
         }

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 3
+#define DD_ABI_VERSION 4
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -286,6 +286,26 @@ int dd_mlp_pack(const DDMlpParams *params, float *packed, void *stream);
 /* Forward pass; out_dim must match the packed parameters. */
 int dd_mlp_forward(const float *packed, int32_t out_dim, const DDMlpIO *io,
                    int64_t n, void *stream);
+
+/* ---- Rendering -------------------------------------
+ * DroneGame.render() in 'rgb_array' mode (game_engine.py:300-337): the scene
+ * of platform.py:76-102, drone.py:155-218, _render_hud (game_engine.py:339-384)
+ * and, for a lane that is done, _render_game_over (:386-412), as
+ * surfarray.array3d(screen).transpose(1, 0, 2) gives it: uint8 [H][W][3] with
+ * W x H = world_width x world_height (800 x 600; width a multiple of 4).
+ * pygame's primitives are restated (render.hip's header), not pixel-verified:
+ * pygame is absent here, and the text uses DejaVu Sans Bold for pygame's
+ * bundled font. */
+enum { DD_RENDER_HUD = 1, DD_RENDER_GAME_OVER = 2 };
+
+/* Renders `count` frames into rgb: uint8 [count][H][W][3].  lanes: int32
+ * [count] device indices into the SoA (each < N, caller-checked), or NULL for
+ * lanes 0..count-1 (count <= N).  actions (nullable): the uint8 [N] bitmask of
+ * the last step, which _render_thrust draws as flames (drone.py:189-218,
+ * where fuel > 0); NULL draws none, as after a reset.  flags: DD_RENDER_*. */
+int dd_render(const DDConfig *cfg, const DDState *st, const uint8_t *actions,
+              const int32_t *lanes, int64_t count, uint8_t *rgb, int32_t flags,
+              void *stream);
 
 /* Algorithmic HBM bytes of one dd_step lane (the roofline byte model,
  * DESIGN.md §4): precision, action format, obs on/off. */

@@ -276,7 +276,11 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     s.y += s.vy * c.dt;
     s.angle += s.omega * c.dt;
     s.omega *= c.angular_drag;
+#ifdef DD_EXP_STEP_WRAP_SELECT
+    s.angle = wrap_angle(s.angle);
+#else
     s.angle = kFlat ? wrap_angle(s.angle) : trig::normalize_angle(s.angle);
+#endif
 
     if (!kRef && sw.platform_moving) {
         const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
@@ -567,12 +571,22 @@ struct Raw {
 
 template <typename T, int AFMT>
 __device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, uint32_t i, Raw<T>& r) {
+#ifndef DD_EXP_LATE_ACT
+    // The action is loaded first and pinned below: only the live branch reads
+    // it, and left to itself the compiler sank its load into that branch,
+    // i.e. behind the wait for the status byte: a second memory round trip.
+    r.act = load_action<AFMT>(actions, i);
+#endif
     r.x = at(a.x, i); r.y = at(a.y, i); r.vx = at(a.vx, i); r.vy = at(a.vy, i);
     r.angle = at(a.angle, i); r.omega = at(a.omega, i); r.fuel = at(a.fuel, i);
     r.px = at(a.px, i); r.py = at(a.py, i); r.total = at(a.total, i);
     r.status = at(a.status, i);
     r.steps = at(a.steps, i);
+#ifdef DD_EXP_LATE_ACT
     r.act = load_action<AFMT>(actions, i);
+#else
+    asm volatile("" ::"v"(r.act));  // every load is issued; this waits for the oldest only
+#endif
 }
 
 // Everything after the loads for one lane: the frame (or sticky done / auto

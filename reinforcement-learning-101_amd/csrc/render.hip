@@ -1,0 +1,385 @@
+// render.hip — dd_render: the rgb_array frame of DroneGame.render
+// (reference delivery_drone/game/game_engine.py:300-337) for a batch of lanes.
+//
+// The reference draws with pygame: sky fill, ground rect (:312-315),
+// Platform.render (platform.py:76-102), Drone.render + _render_thrust
+// (drone.py:155-218), _render_hud (game_engine.py:339-384) and, once the
+// game is over, _render_game_over (:386-412); rgb_array mode returns
+// surfarray.array3d(screen).transpose(1, 0, 2), i.e. [H][W][3] uint8.  Here a
+// frame is one pass of a per-pixel kernel that evaluates the same scene in
+// painter's order for 4 consecutive pixels per lane (12 output bytes), one
+// grid row per rendered lane, so the lane's state is wave-uniform (scalar
+// loads) and the frame leaves as contiguous stores: the kernel is bound by
+// the bytes it writes (1.44 MB per 800 x 600 frame).
+//
+// pygame is not installed here, so these are restatements of its primitive
+// rules, not pixel-verified against it ("Rendering"):
+//   * rect (l, t, w, h): pixels l <= X < l + w, t <= Y < t + h; an outline of
+//     width 2 is the rect's pixels within 2 of an edge;
+//   * a vertical line of width 2 from (cx, t) to (cx, b): columns cx, cx + 1,
+//     rows t..b inclusive;
+//   * filled circle (c, r): (X - cx)^2 + (Y - cy)^2 <= r^2; filled ellipse in
+//     rect (l, t, w, h): pixel centres inside the inscribed ellipse;
+//   * transform.rotate(surface, -angle) + blit centred on (x, y): every pixel
+//     centre is rotated back into the 40 x 20 drone sprite and takes the
+//     sprite pixel it lands on (nearest neighbour), transparent outside;
+//   * text: pygame.font.Font(None, 24 | 30 | 48) is stood in for by DejaVu
+//     Sans Bold at 16 / 20 / 33 px (font_atlas.h); anti-aliased glyph
+//     coverage a blends as pygame's ALPHA_BLEND: d += ((s - d) * a + s) >> 8;
+//   * the game-over overlay (surface alpha 128, black): d += (-d * 128) >> 8.
+// Geometry of the rotated parts is computed in float32 from float32-rounded
+// sin / cos of the angle, so the CPU restatement (oracle/render.py) gets the
+// same pixels; numbers in the HUD are formatted like Python's f-strings
+// (correctly rounded, ties to even).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dronestep.h"
+#include "font_atlas.h"
+#include "trig.h"
+
+namespace dd {
+namespace render {
+
+constexpr int kBlock = 256;
+constexpr int kPix = 4;  // pixels per lane
+constexpr int kTexts = 10;
+constexpr int kMaxChars = 32;
+constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
+
+// colours, 0x00BBGGRR (config.py:9-15 and the literals of the render code)
+__host__ __device__ constexpr uint32_t rgb(uint32_t r, uint32_t g, uint32_t b) { return r | (g << 8) | (b << 16); }
+constexpr uint32_t kSky = rgb(135, 206, 235), kGround = rgb(101, 67, 33), kPlatform = rgb(50, 205, 50),
+                   kOutline = rgb(0, 150, 0), kWhite = rgb(255, 255, 255), kDrone = rgb(200, 200, 200),
+                   kRotor = rgb(100, 100, 100), kHub = rgb(50, 50, 50), kThrust = rgb(255, 100, 0),
+                   kBarBg = rgb(50, 50, 50), kGreen = rgb(0, 255, 0), kYellow = rgb(255, 255, 0),
+                   kRed = rgb(255, 0, 0);
+constexpr int kDroneW = 40;  // config.DRONE_WIDTH (the sprite; the physics never reads it)
+
+struct Text {
+    int32_t x0, y0, w, h, face, len;
+    uint32_t color;
+    uint8_t s[kMaxChars];
+};
+
+// ---- f-string formatting (Python's int() / str(int) / format(x, '.Nf')) ----
+struct Str {
+    uint8_t* c;
+    int n;
+    __device__ void put(char ch) {
+        if (n < kMaxChars) c[n++] = (uint8_t)ch;
+    }
+    __device__ void put(const char* lit) {
+        while (*lit) put(*lit++);
+    }
+    __device__ void put_u64(uint64_t v) {
+        char tmp[20];
+        int k = 0;
+        do { tmp[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+        while (k) put(tmp[--k]);
+    }
+    __device__ void put_i64(int64_t v) {
+        if (v < 0) { put('-'); put_u64((uint64_t)(-(v + 1)) + 1u); } else { put_u64((uint64_t)v); }
+    }
+    // format(x, '.1f') / '.0f': the correctly rounded decimal, ties to even,
+    // "-" for a set sign bit (Python prints -0.0 as "-0.0").  x * 10 is split
+    // into its rounded product p and the exact remainder e = fma(x, 10, -p),
+    // so a tie of p is resolved by the sign of e.  |x| >= 2^50 prints the
+    // integer part only (never reached by a frame's values).
+    __device__ void put_fixed(double x, int decimals) {
+        if (__builtin_isnan(x)) { put("nan"); return; }
+        if (__builtin_signbit(x)) put('-');
+        x = fabs(x);
+        if (__builtin_isinf(x)) { put("inf"); return; }
+        if (x >= 1125899906842624.0) { put_u64((uint64_t)x); return; }
+        const double scale = decimals ? 10.0 : 1.0;
+        const double p = x * scale;
+        const double e = fma(x, scale, -p);
+        double r = rint(p);
+        const double d = p - r;
+        if (d == 0.5 && e > 0.0) r += 1.0;
+        else if (d == -0.5 && e < 0.0) r -= 1.0;
+        const uint64_t q = (uint64_t)r;
+        if (decimals) { put_u64(q / 10); put('.'); put((char)('0' + q % 10)); } else { put_u64(q); }
+    }
+};
+
+__device__ __forceinline__ int text_width(int face, const uint8_t* s, int len) {
+    int w = 0;
+    for (int k = 0; k < len; ++k) {
+        const int g = font::kIndex[face * 128 + (s[k] & 127)];
+        if (g >= 0) w += font::kAdvance[g];
+    }
+    return w;
+}
+
+// pygame's per-pixel-alpha blit: d += ((s - d) * a + s) >> 8, per channel
+__device__ __forceinline__ uint32_t blend(uint32_t d, uint32_t s, int a) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const int dc = (int)((d >> (8 * ch)) & 255u), sc = (int)((s >> (8 * ch)) & 255u);
+        out |= (uint32_t)(dc + (((sc - dc) * a + sc) >> 8)) << (8 * ch);
+    }
+    return out;
+}
+
+// the game-over overlay: black at surface alpha 128
+__device__ __forceinline__ uint32_t darken(uint32_t d) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const int dc = (int)((d >> (8 * ch)) & 255u);
+        out |= (uint32_t)(dc + ((-dc * 128) >> 8)) << (8 * ch);
+    }
+    return out;
+}
+
+// coverage of text t at pixel (X, Y), 0 outside it
+__device__ __forceinline__ int text_cover(const Text& t, int X, int Y) {
+    const int u = X - t.x0, v = Y - t.y0;
+    if (u < 0 || u >= t.w || v < 0 || v >= t.h) return 0;
+    int base = 0;
+    for (int k = 0; k < t.len; ++k) {
+        const int g = font::kIndex[t.face * 128 + (t.s[k] & 127)];
+        if (g < 0) continue;
+        const int adv = font::kAdvance[g];
+        if (u < base + adv) return font::kAtlas[font::kOffset[g] + v * adv + (u - base)];
+        base += adv;
+    }
+    return 0;
+}
+
+struct Args {
+    const uint8_t* actions;  // [N] bitmask of the last step (nullable: no flames)
+    const int32_t* lanes;    // [count] lanes to draw (nullable: 0..count-1)
+    uint8_t* rgb;            // [count][H][W][3]
+    int32_t width, height, ground, count;
+    int32_t phw, phh, dhh;   // platform half width / height, drone half height (px)
+    int32_t flags;
+};
+
+template <typename T>
+struct View {
+    const T *x, *y, *vx, *vy, *angle, *fuel, *px, *py, *total;
+    const uint8_t* status;
+    const int32_t *steps, *episode;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
+    __shared__ Text texts[kTexts];
+    const int slot = blockIdx.y;
+    const int lane = p.lanes ? p.lanes[slot] : slot;
+    // the lane's state: wave-uniform
+    const double x = (double)v.x[lane], y = (double)v.y[lane], angle = (double)v.angle[lane];
+    const double fuel = (double)v.fuel[lane], px = (double)v.px[lane], py = (double)v.py[lane];
+    const uint32_t status = v.status[lane];
+    const uint32_t act = p.actions ? p.actions[lane] : 0u;
+    const int W = p.width, H = p.height;
+    const int first = (blockIdx.x * kBlock) * kPix;  // this block's first pixel
+    const int row_lo = first / W, row_hi = min(H - 1, (first + kBlock * kPix - 1) / W);
+
+    // float32 geometry of the rotated parts (see the header)
+    double sd, cd;
+    trig::sincos(angle * kDeg2Rad, &sd, &cd);
+    const float s = (float)sd, c = (float)cd;
+    const float xf = (float)x, yf = (float)y;
+    const float hw = 0.5f * kDroneW, hh = (float)p.dhh;
+    // _render_thrust flame centres: rotate_point(...) then int(x + fx), int(y + fy)
+    const bool lit = fuel > 0.0;
+    const bool main_on = (act & 1u) && lit, left_on = (act & 2u) && lit, right_on = (act & 4u) && lit;
+    const float fl = hh + 15.0f / 2.0f;  // height / 2 + flame_length / 2
+    const int mx = (int)(xf + (0.0f * c - fl * s)), my = (int)(yf + (0.0f * s + fl * c));
+    const float sl = hw + 10.0f / 2.0f;  // width / 2 + side_flame_length / 2
+    const int lx = (int)(xf + (-sl * c - 0.0f * s)), ly = (int)(yf + (-sl * s + 0.0f * c));
+    const int rx = (int)(xf + (sl * c - 0.0f * s)), ry = (int)(yf + (sl * s + 0.0f * c));
+    // platform bounds (platform.py:51-62), pygame truncating the float rect
+    const int pl = (int)(px - p.phw), pt = (int)(py - p.phh), pw = 2 * p.phw, ph = 2 * p.phh;
+    const int pcx = (int)px, pby = (int)(py + p.phh);
+    const bool hud = p.flags & DD_RENDER_HUD;
+    const bool over = (p.flags & DD_RENDER_GAME_OVER) && (status & DD_ST_DONE);
+
+    // Text rows: the HUD (y 10..~110), the pad's "H", the game-over lines.
+    // Blocks whose rows meet one format every string (threads 0..9).
+    const int hlo = pt - 40, hhi = pt + ph + 40;
+    const bool need_text = (hud && row_lo < 130) || (row_hi >= hlo && row_lo <= hhi) ||
+                           (over && row_hi >= H / 2 - 60 && row_lo <= H / 2 + 70);
+    if (need_text) {
+        const int k = threadIdx.x;
+        if (k < kTexts) {
+            Text& t = texts[k];
+            Str str{t.s, 0};
+            int face = 0, cx = -1, cy = 0, x0 = 0, y0 = 0;
+            uint32_t color = kWhite;
+            bool on = hud;
+            switch (k) {
+                case 0:  // f"Fuel: {int(self.drone.fuel)}" at (15, 12)
+                    str.put("Fuel: "); str.put_i64((int64_t)fuel); x0 = 15; y0 = 12; break;
+                case 1: {  // f"Speed: {get_speed():.1f}" at (10, 40)
+                    const double vx = (double)v.vx[lane], vy = (double)v.vy[lane];
+                    str.put("Speed: "); str.put_fixed(sqrt(vx * vx + vy * vy), 1); x0 = 10; y0 = 40; break;
+                }
+                case 2:  // f"Angle: {angle:.1f}°" at (10, 65)
+                    str.put("Angle: "); str.put_fixed(angle, 1); str.put((char)font::kDegree); x0 = 10; y0 = 65; break;
+                case 3: {  // f"Distance: {distance:.0f}" at (10, 90)
+                    const double dx = px - x, dy = py - y;
+                    str.put("Distance: "); str.put_fixed(sqrt(dx * dx + dy * dy), 0); x0 = 10; y0 = 90; break;
+                }
+                case 4:  // f"Episode: {episode}" at (W - 150, 10)
+                    str.put("Episode: "); str.put_i64(v.episode[lane]); x0 = W - 150; y0 = 10; break;
+                case 5:  // f"Steps: {steps}" at (W - 150, 35)
+                    str.put("Steps: "); str.put_i64(v.steps[lane]); x0 = W - 150; y0 = 35; break;
+                case 6:  // the pad's "H", centred on (int(x), int(y))
+                    str.put("H"); face = 1; cx = pcx; cy = (int)py; on = true; break;
+                case 7:  // game-over title, centred on (W // 2, H // 2 - 30)
+                    if (status & DD_ST_LANDED) { str.put("SUCCESSFUL LANDING!"); color = kGreen; }
+                    else { str.put("CRASHED!"); color = kRed; }
+                    face = 2; cx = W / 2; cy = H / 2 - 30; on = over; break;
+                case 8:  // f"Total Reward: {total_reward:.1f}", centred on (W // 2, H // 2 + 20)
+                    str.put("Total Reward: "); str.put_fixed((double)v.total[lane], 1);
+                    cx = W / 2; cy = H / 2 + 20; on = over; break;
+                default:  // "Press R to restart", centred on (W // 2, H // 2 + 50)
+                    str.put("Press R to restart"); cx = W / 2; cy = H / 2 + 50; on = over; break;
+            }
+            t.len = on ? str.n : 0;
+            t.face = face;
+            t.color = color;
+            t.h = font::kHeight[face];
+            t.w = text_width(face, t.s, t.len);
+            if (cx >= 0) {  // get_rect(center=...): x = cx - w // 2, y = cy - h // 2
+                x0 = cx - t.w / 2;
+                y0 = cy - t.h / 2;
+            }
+            t.x0 = x0;
+            t.y0 = y0;
+        }
+        __syncthreads();
+    }
+
+    const int t0 = blockIdx.x * kBlock + threadIdx.x;
+    if (t0 * kPix >= W * H) return;
+    const int Y = (t0 * kPix) / W, X0 = (t0 * kPix) - Y * W;
+    const int fuel_w = (int)(200.0 * (fuel / 1000.0));  // fuel_bar_width * fuel_percent
+    const double fpct = fuel / 1000.0;
+    const uint32_t fuel_color = fpct > 0.3 ? kGreen : fpct > 0.1 ? kYellow : kRed;
+    uint32_t px4[kPix];
+#pragma unroll
+    for (int j = 0; j < kPix; ++j) {
+        const int X = X0 + j;
+        uint32_t col = Y >= p.ground ? kGround : kSky;
+        // Platform.render: fill, 2-px outline, centre line, "H"
+        if (X >= pl && X < pl + pw && Y >= pt && Y < pt + ph) {
+            const bool edge = X < pl + 2 || X >= pl + pw - 2 || Y < pt + 2 || Y >= pt + ph - 2;
+            col = edge ? kOutline : kPlatform;
+        }
+        if ((X == pcx || X == pcx + 1) && Y >= pt && Y <= pby) col = kWhite;
+        if (need_text) {
+            const int a = text_cover(texts[6], X, Y);
+            if (a) col = blend(col, texts[6].color, a);
+        }
+        // Drone.render: the sprite rotated about (x, y), nearest neighbour
+        const float dx = ((float)X + 0.5f) - xf, dy = ((float)Y + 0.5f) - yf;
+        if (fabsf(dx) <= hw + hh + 1.0f && fabsf(dy) <= hw + hh + 1.0f) {
+            const float u = dx * c + dy * s, w = dy * c - dx * s;
+            const float su = floorf(u + hw), sv = floorf(w + hh);
+            if (su >= 0.0f && su < (float)kDroneW && sv >= 0.0f && sv < 2.0f * hh) {
+                const int i = (int)su, k = (int)sv, cy = (int)hh;  // rotor / hub centres at height // 2
+                const int d0 = (i - kDroneW / 2) * (i - kDroneW / 2) + (k - cy) * (k - cy);
+                const int d1 = (i - 5) * (i - 5) + (k - cy) * (k - cy);
+                const int d2 = (i - (kDroneW - 5)) * (i - (kDroneW - 5)) + (k - cy) * (k - cy);
+                col = d0 <= 9 ? kHub : (d1 <= 25 || d2 <= 25) ? kRotor : kDrone;
+            }
+        }
+        // _render_thrust: main flame ellipse (fx - 8, fy - 7, 16, 15), side circles r = 5
+        if (main_on) {
+            const float ex = ((float)X + 0.5f - (float)mx) / 8.0f;
+            const float ey = ((float)Y + 0.5f - ((float)(my - 7) + 7.5f)) / 7.5f;
+            if (ex * ex + ey * ey <= 1.0f) col = kThrust;
+        }
+        if (left_on && (X - lx) * (X - lx) + (Y - ly) * (Y - ly) <= 25) col = kThrust;
+        if (right_on && (X - rx) * (X - rx) + (Y - ry) * (Y - ry) <= 25) col = kThrust;
+        // _render_hud
+        if (hud && Y < 130) {
+            if (X >= 10 && X < 210 && Y >= 10 && Y < 30) col = X < 10 + fuel_w ? fuel_color : kBarBg;
+#pragma unroll 1
+            for (int k = 0; k < 6; ++k) {
+                const int a = text_cover(texts[k], X, Y);
+                if (a) col = blend(col, texts[k].color, a);
+            }
+        }
+        // _render_game_over
+        if (over) {
+            col = darken(col);
+            if (need_text) {
+#pragma unroll 1
+                for (int k = 7; k < kTexts; ++k) {
+                    const int a = text_cover(texts[k], X, Y);
+                    if (a) col = blend(col, texts[k].color, a);
+                }
+            }
+        }
+        px4[j] = col;
+    }
+    // 4 RGB pixels = 3 dwords, little-endian byte order R G B R G B ...
+    const uint32_t w0 = (px4[0] & 0xFFFFFFu) | (px4[1] << 24);
+    const uint32_t w1 = ((px4[1] >> 8) & 0xFFFFu) | (px4[2] << 16);
+    const uint32_t w2 = ((px4[2] >> 16) & 0xFFu) | (px4[3] << 8);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(p.rgb + ((size_t)slot * W * H + (size_t)t0 * kPix) * 3);
+    __builtin_nontemporal_store(w0, dst);
+    __builtin_nontemporal_store(w1, dst + 1);
+    __builtin_nontemporal_store(w2, dst + 2);
+}
+
+template <typename T>
+View<T> view_of(const DDState& st) {
+    View<T> v;
+    v.x = (const T*)st.x; v.y = (const T*)st.y; v.vx = (const T*)st.vx; v.vy = (const T*)st.vy;
+    v.angle = (const T*)st.angle; v.fuel = (const T*)st.fuel; v.px = (const T*)st.px; v.py = (const T*)st.py;
+    v.total = (const T*)st.total_reward;
+    v.status = st.status; v.steps = st.steps; v.episode = st.episode;
+    return v;
+}
+
+// an integer-valued double in [lo, hi]
+inline bool whole(double d, double lo, double hi) { return d >= lo && d <= hi && d == (double)(int64_t)d; }
+
+}  // namespace render
+}  // namespace dd
+
+extern "C" int dd_render(const DDConfig* cfg, const DDState* st, const uint8_t* actions, const int32_t* lanes,
+                         int64_t count, uint8_t* rgb, int32_t flags, void* stream) {
+    using namespace dd::render;
+    if (!cfg || !st || count < 0) return (int)hipErrorInvalidValue;
+    if (count == 0) return 0;
+    if (!rgb || !st->x || !st->y || !st->vx || !st->vy || !st->angle || !st->fuel || !st->px || !st->py ||
+        !st->total_reward || !st->status || !st->steps || !st->episode)
+        return (int)hipErrorInvalidValue;
+    if (!whole(cfg->world_width, 4, 16384) || !whole(cfg->world_height, 1, 16384) ||
+        ((int64_t)cfg->world_width % 4) != 0 || !whole(cfg->ground_level, -1e6, 1e6) ||
+        !whole(cfg->platform_half_width, 0, 4096) || !whole(cfg->platform_half_height, 0, 4096) ||
+        !whole(cfg->drone_half_height, 1, 64) || count > 65535)
+        return (int)hipErrorInvalidValue;
+    Args p;
+    p.actions = actions;
+    p.lanes = lanes;
+    p.rgb = rgb;
+    p.width = (int32_t)cfg->world_width;
+    p.height = (int32_t)cfg->world_height;
+    p.ground = (int32_t)cfg->ground_level;
+    p.count = (int32_t)count;
+    p.phw = (int32_t)cfg->platform_half_width;
+    p.phh = (int32_t)cfg->platform_half_height;
+    p.dhh = (int32_t)cfg->drone_half_height;
+    p.flags = flags;
+    const int64_t quads = (int64_t)p.width * p.height / kPix;
+    dim3 grid((unsigned)((quads + kBlock - 1) / kBlock), (unsigned)count);
+    hipStream_t s = (hipStream_t)stream;
+    if (st->precision == DD_F64)
+        render_kernel<double><<<grid, kBlock, 0, s>>>(p, view_of<double>(*st));
+    else if (st->precision == DD_F32)
+        render_kernel<float><<<grid, kBlock, 0, s>>>(p, view_of<float>(*st));
+    else
+        return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+}

@@ -202,16 +202,18 @@ class DroneGameClient:
 class DroneGame:
     """One game with the engine API of ``DroneGame`` (game_engine.py:11-298).
 
-    ``render_mode`` must be None: rendering is out of scope for this path.
+    ``render_mode`` is None (headless) or ``'rgb_array'`` (``render()``
+    returns the frame as a numpy uint8 [600, 800, 3], drawn on the GPU by
+    dd_render); ``'human'`` needs a pygame window and is not supported.
     Defaults to ``precision="f64"`` so a single game tracks the reference's
     double-precision trajectory.
     """
 
     def __init__(self, render_mode=None, randomize_drone: bool = False, randomize_platform: bool = True, *,
                  seed: int = 0, device=None, precision: str = "f64", config=None, env_id: int = 0):
-        if render_mode is not None:
-            raise NotImplementedError("rendering is out of scope; use render_mode=None")
-        self.render_mode = None
+        if render_mode not in (None, "rgb_array"):
+            raise NotImplementedError("render_mode='human' needs a display; use None or 'rgb_array'")
+        self.render_mode = render_mode
         self.env = VecDroneEnv(1, randomize_drone=randomize_drone, randomize_platform=randomize_platform,
                                auto_reset=False, seed=seed, device=device, precision=precision,
                                config=config, env_id_base=env_id)
@@ -246,7 +248,10 @@ class DroneGame:
         return self._lanes.info(0)
 
     def render(self):
-        return None
+        """game_engine.py:300-337: None headless, else the rgb_array frame."""
+        if self.render_mode is None:
+            return None
+        return self.env.render(lanes=0)[0].cpu().numpy()
 
     def close(self):
         pass

@@ -37,6 +37,8 @@ for v in ${VARIANTS:-base}; do
     w4) build w4 -DDD_STEP_MIN_WAVES=4 ;;
     rw2) build rw2 -DDD_ROLL_MIN_WAVES=2 ;;
     rw4) build rw4 -DDD_ROLL_MIN_WAVES=4 ;;
+    lateact) build lateact -DDD_EXP_LATE_ACT ;;
+    wrapsel) build wrapsel -DDD_EXP_STEP_WRAP_SELECT ;;
     *) echo "unknown variant $v" >&2; exit 1 ;;
   esac
 done
