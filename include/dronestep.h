@@ -298,14 +298,15 @@ int dd_mlp_forward(const float *packed, int32_t out_dim, const DDMlpIO *io,
  * bundled font. */
 enum { DD_RENDER_HUD = 1, DD_RENDER_GAME_OVER = 2 };
 
-/* Renders `count` frames into rgb: uint8 [count][H][W][3].  lanes: int32
- * [count] device indices into the SoA (each < N, caller-checked), or NULL for
- * lanes 0..count-1 (count <= N).  actions (nullable): the uint8 [N] bitmask of
- * the last step, which _render_thrust draws as flames (drone.py:189-218,
- * where fuel > 0); NULL draws none, as after a reset.  flags: DD_RENDER_*. */
+/* Renders `count` frames into rgb: uint8 [count][H][W][3].  The SoA holds n
+ * lanes.  lanes: int32 [count] device indices into it, or NULL for lanes
+ * 0..count-1 (count <= n); a frame whose index is outside [0, n) is left
+ * all zero.  actions (nullable): the uint8 [n] bitmask of the last step, which
+ * _render_thrust draws as flames (drone.py:189-218, where fuel > 0); NULL
+ * draws none, as after a reset.  flags: DD_RENDER_*. */
 int dd_render(const DDConfig *cfg, const DDState *st, const uint8_t *actions,
-              const int32_t *lanes, int64_t count, uint8_t *rgb, int32_t flags,
-              void *stream);
+              const int32_t *lanes, int64_t count, int64_t n, uint8_t *rgb,
+              int32_t flags, void *stream);
 
 /* Algorithmic HBM bytes of one dd_step lane (the roofline byte model,
  * DESIGN.md §4): precision, action format, obs on/off. */

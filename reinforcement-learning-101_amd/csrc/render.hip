@@ -56,10 +56,15 @@ constexpr uint32_t kSky = rgb(135, 206, 235), kGround = rgb(101, 67, 33), kPlatf
                    kRed = rgb(255, 0, 0);
 constexpr int kDroneW = 40;  // config.DRONE_WIDTH (the sprite; the physics never reads it)
 
+// One string of the frame, laid out: its chars, the glyph and left edge of
+// each, and (built per block) the char under every column of its box.
+constexpr int kMaxTextW = 640;
 struct Text {
     int32_t x0, y0, w, h, face, len;
     uint32_t color;
     uint8_t s[kMaxChars];
+    int16_t glyph[kMaxChars];
+    int16_t start[kMaxChars];
 };
 
 // ---- f-string formatting (Python's int() / str(int) / format(x, '.Nf')) ----
@@ -75,7 +80,9 @@ struct Str {
     __device__ void put_u64(uint64_t v) {
         char tmp[20];
         int k = 0;
-        do { tmp[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+        while (v >> 32) { tmp[k++] = (char)('0' + v % 10); v /= 10; }  // 64-bit division only above 2^32
+        uint32_t w = (uint32_t)v;
+        do { tmp[k++] = (char)('0' + w % 10u); w /= 10u; } while (w);
         while (k) put(tmp[--k]);
     }
     __device__ void put_i64(int64_t v) {
@@ -104,15 +111,6 @@ struct Str {
     }
 };
 
-__device__ __forceinline__ int text_width(int face, const uint8_t* s, int len) {
-    int w = 0;
-    for (int k = 0; k < len; ++k) {
-        const int g = font::kIndex[face * 128 + (s[k] & 127)];
-        if (g >= 0) w += font::kAdvance[g];
-    }
-    return w;
-}
-
 // pygame's per-pixel-alpha blit: d += ((s - d) * a + s) >> 8, per channel
 __device__ __forceinline__ uint32_t blend(uint32_t d, uint32_t s, int a) {
     uint32_t out = 0;
@@ -135,19 +133,26 @@ __device__ __forceinline__ uint32_t darken(uint32_t d) {
     return out;
 }
 
-// coverage of text t at pixel (X, Y), 0 outside it
-__device__ __forceinline__ int text_cover(const Text& t, int X, int Y) {
+// The font tables a block reads while laying out and drawing its strings,
+// copied to LDS once (the layout walks them char by char: from global
+// memory that was a chain of dependent loads per string).
+struct FontLds {
+    int16_t index[font::kFaces * 128];
+    uint8_t advance[font::kGlyphs];
+    uint32_t offset[font::kGlyphs];
+};
+
+// string t blended over colour d at pixel (X, Y) (pygame ALPHA_BLEND of the
+// glyph's coverage); d unchanged outside its box
+__device__ __forceinline__ uint32_t draw_text(uint32_t d, const Text& t, const uint8_t* cc, const FontLds& fl,
+                                              int X, int Y) {
     const int u = X - t.x0, v = Y - t.y0;
-    if (u < 0 || u >= t.w || v < 0 || v >= t.h) return 0;
-    int base = 0;
-    for (int k = 0; k < t.len; ++k) {
-        const int g = font::kIndex[t.face * 128 + (t.s[k] & 127)];
-        if (g < 0) continue;
-        const int adv = font::kAdvance[g];
-        if (u < base + adv) return font::kAtlas[font::kOffset[g] + v * adv + (u - base)];
-        base += adv;
-    }
-    return 0;
+    if (u < 0 || u >= t.w || v < 0 || v >= t.h || t.len == 0) return d;
+    const int i = cc[u];
+    const int g = t.glyph[i];
+    const int adv = fl.advance[g];
+    const int a = font::kAtlas[fl.offset[g] + v * adv + (u - t.start[i])];
+    return a ? blend(d, t.color, a) : d;
 }
 
 struct Args {
@@ -155,6 +160,7 @@ struct Args {
     const int32_t* lanes;    // [count] lanes to draw (nullable: 0..count-1)
     uint8_t* rgb;            // [count][H][W][3]
     int32_t width, height, ground, count;
+    int64_t n;               // lanes in the SoA
     int32_t phw, phh, dhh;   // platform half width / height, drone half height (px)
     int32_t flags;
 };
@@ -169,8 +175,20 @@ struct View {
 template <typename T>
 __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     __shared__ Text texts[kTexts];
+    __shared__ uint8_t colchar[kTexts][kMaxTextW];
+    __shared__ FontLds fl;
     const int slot = blockIdx.y;
     const int lane = p.lanes ? p.lanes[slot] : slot;
+    if (lane < 0 || lane >= p.n) {  // not a lane: an all-zero frame
+        const int t = blockIdx.x * kBlock + threadIdx.x;
+        if (t * kPix < p.width * p.height) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(p.rgb + ((size_t)slot * p.width * p.height + (size_t)t * kPix) * 3);
+            __builtin_nontemporal_store(0u, dst);
+            __builtin_nontemporal_store(0u, dst + 1);
+            __builtin_nontemporal_store(0u, dst + 2);
+        }
+        return;
+    }
     // the lane's state: wave-uniform
     const double x = (double)v.x[lane], y = (double)v.y[lane], angle = (double)v.angle[lane];
     const double fuel = (double)v.fuel[lane], px = (double)v.px[lane], py = (double)v.py[lane];
@@ -189,8 +207,8 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     // _render_thrust flame centres: rotate_point(...) then int(x + fx), int(y + fy)
     const bool lit = fuel > 0.0;
     const bool main_on = (act & 1u) && lit, left_on = (act & 2u) && lit, right_on = (act & 4u) && lit;
-    const float fl = hh + 15.0f / 2.0f;  // height / 2 + flame_length / 2
-    const int mx = (int)(xf + (0.0f * c - fl * s)), my = (int)(yf + (0.0f * s + fl * c));
+    const float flame = hh + 15.0f / 2.0f;  // height / 2 + flame_length / 2
+    const int mx = (int)(xf + (0.0f * c - flame * s)), my = (int)(yf + (0.0f * s + flame * c));
     const float sl = hw + 10.0f / 2.0f;  // width / 2 + side_flame_length / 2
     const int lx = (int)(xf + (-sl * c - 0.0f * s)), ly = (int)(yf + (-sl * s + 0.0f * c));
     const int rx = (int)(xf + (sl * c - 0.0f * s)), ry = (int)(yf + (sl * s + 0.0f * c));
@@ -200,59 +218,107 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     const bool hud = p.flags & DD_RENDER_HUD;
     const bool over = (p.flags & DD_RENDER_GAME_OVER) && (status & DD_ST_DONE);
 
-    // Text rows: the HUD (y 10..~110), the pad's "H", the game-over lines.
-    // Blocks whose rows meet one format every string (threads 0..9).
-    const int hlo = pt - 40, hhi = pt + ph + 40;
-    const bool need_text = (hud && row_lo < 130) || (row_hi >= hlo && row_lo <= hhi) ||
-                           (over && row_hi >= H / 2 - 60 && row_lo <= H / 2 + 70);
-    if (need_text) {
+    // Block culling: a block covers kBlock * kPix = 1,024 pixels (1-2 rows),
+    // so each group of primitives is tested against the block's rows once
+    // (a scalar branch) and most blocks only fill sky or ground.
+    //   pad band: the platform and its centre line (pt .. bottom);
+    //   drone band: the sprite (radius 22.4) and the flames (<= 30 px out);
+    //   strings: only those whose rows meet the block's are laid out.
+    const bool blk_pad = row_hi >= pt && row_lo <= pby;
+    const bool blk_drone = (float)row_hi + 48.0f >= yf && (float)row_lo - 48.0f <= yf;
+    // string k: where (y0 follows from the face height alone) and whether it is drawn
+    int tx[kTexts], ty[kTexts], tface[kTexts];
+    bool ton[kTexts], tcentre[kTexts];
+    {
+        const int hud_y[6] = {12, 40, 65, 90, 10, 35};
+        const int hud_x[6] = {15, 10, 10, 10, W - 150, W - 150};
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            tx[k] = hud_x[k]; ty[k] = hud_y[k]; tface[k] = 0; ton[k] = hud; tcentre[k] = false;
+        }
+        tx[6] = pcx; ty[6] = (int)py; tface[6] = 1; ton[6] = true; tcentre[6] = true;  // the pad's "H"
+        const int over_y[3] = {H / 2 - 30, H / 2 + 20, H / 2 + 50};
+#pragma unroll
+        for (int k = 7; k < kTexts; ++k) {
+            tx[k] = W / 2; ty[k] = over_y[k - 7]; tface[k] = k == 7 ? 2 : 0; ton[k] = over; tcentre[k] = true;
+        }
+    }
+    uint32_t need = 0;  // strings this block draws (wave-uniform)
+#pragma unroll
+    for (int k = 0; k < kTexts; ++k) {
+        const int h = font::kHeight[tface[k]];
+        const int y0 = tcentre[k] ? ty[k] - h / 2 : ty[k];
+        if (ton[k] && row_hi >= y0 && row_lo < y0 + h) need |= 1u << k;
+    }
+    if (need) {
+        for (int i = threadIdx.x; i < font::kFaces * 128; i += kBlock) fl.index[i] = font::kIndex[i];
+        for (int i = threadIdx.x; i < font::kGlyphs; i += kBlock) {
+            fl.advance[i] = font::kAdvance[i];
+            fl.offset[i] = font::kOffset[i];
+        }
+        __syncthreads();
         const int k = threadIdx.x;
-        if (k < kTexts) {
+        if (k < kTexts && ((need >> k) & 1u)) {
             Text& t = texts[k];
             Str str{t.s, 0};
-            int face = 0, cx = -1, cy = 0, x0 = 0, y0 = 0;
             uint32_t color = kWhite;
-            bool on = hud;
             switch (k) {
                 case 0:  // f"Fuel: {int(self.drone.fuel)}" at (15, 12)
-                    str.put("Fuel: "); str.put_i64((int64_t)fuel); x0 = 15; y0 = 12; break;
+                    str.put("Fuel: "); str.put_i64((int64_t)fuel); break;
                 case 1: {  // f"Speed: {get_speed():.1f}" at (10, 40)
                     const double vx = (double)v.vx[lane], vy = (double)v.vy[lane];
-                    str.put("Speed: "); str.put_fixed(sqrt(vx * vx + vy * vy), 1); x0 = 10; y0 = 40; break;
+                    str.put("Speed: "); str.put_fixed(sqrt(vx * vx + vy * vy), 1); break;
                 }
                 case 2:  // f"Angle: {angle:.1f}°" at (10, 65)
-                    str.put("Angle: "); str.put_fixed(angle, 1); str.put((char)font::kDegree); x0 = 10; y0 = 65; break;
+                    str.put("Angle: "); str.put_fixed(angle, 1); str.put((char)font::kDegree); break;
                 case 3: {  // f"Distance: {distance:.0f}" at (10, 90)
                     const double dx = px - x, dy = py - y;
-                    str.put("Distance: "); str.put_fixed(sqrt(dx * dx + dy * dy), 0); x0 = 10; y0 = 90; break;
+                    str.put("Distance: "); str.put_fixed(sqrt(dx * dx + dy * dy), 0); break;
                 }
                 case 4:  // f"Episode: {episode}" at (W - 150, 10)
-                    str.put("Episode: "); str.put_i64(v.episode[lane]); x0 = W - 150; y0 = 10; break;
+                    str.put("Episode: "); str.put_i64(v.episode[lane]); break;
                 case 5:  // f"Steps: {steps}" at (W - 150, 35)
-                    str.put("Steps: "); str.put_i64(v.steps[lane]); x0 = W - 150; y0 = 35; break;
+                    str.put("Steps: "); str.put_i64(v.steps[lane]); break;
                 case 6:  // the pad's "H", centred on (int(x), int(y))
-                    str.put("H"); face = 1; cx = pcx; cy = (int)py; on = true; break;
+                    str.put("H"); break;
                 case 7:  // game-over title, centred on (W // 2, H // 2 - 30)
                     if (status & DD_ST_LANDED) { str.put("SUCCESSFUL LANDING!"); color = kGreen; }
                     else { str.put("CRASHED!"); color = kRed; }
-                    face = 2; cx = W / 2; cy = H / 2 - 30; on = over; break;
+                    break;
                 case 8:  // f"Total Reward: {total_reward:.1f}", centred on (W // 2, H // 2 + 20)
-                    str.put("Total Reward: "); str.put_fixed((double)v.total[lane], 1);
-                    cx = W / 2; cy = H / 2 + 20; on = over; break;
+                    str.put("Total Reward: "); str.put_fixed((double)v.total[lane], 1); break;
                 default:  // "Press R to restart", centred on (W // 2, H // 2 + 50)
-                    str.put("Press R to restart"); cx = W / 2; cy = H / 2 + 50; on = over; break;
+                    str.put("Press R to restart"); break;
             }
-            t.len = on ? str.n : 0;
+            const int face = tface[k];
+            int w = 0, n = 0;
+            for (int i = 0; i < str.n; ++i) {  // glyphs with a cell in this face, side by side
+                const int g = fl.index[face * 128 + (t.s[i] & 127)];
+                if (g < 0) continue;
+                t.glyph[n] = (int16_t)g;
+                t.start[n] = (int16_t)w;
+                w += fl.advance[g];
+                ++n;
+            }
+            t.len = n;
             t.face = face;
             t.color = color;
             t.h = font::kHeight[face];
-            t.w = text_width(face, t.s, t.len);
-            if (cx >= 0) {  // get_rect(center=...): x = cx - w // 2, y = cy - h // 2
-                x0 = cx - t.w / 2;
-                y0 = cy - t.h / 2;
+            t.w = min(w, kMaxTextW);
+            // get_rect(center=...): x = cx - w // 2, y = cy - h // 2
+            t.x0 = tcentre[k] ? tx[k] - w / 2 : tx[k];
+            t.y0 = tcentre[k] ? ty[k] - t.h / 2 : ty[k];
+        }
+        __syncthreads();
+        // the char under every column of each string drawn here
+        for (uint32_t m = need; m; m &= m - 1) {
+            const int k2 = __builtin_ctz(m);
+            const Text& t = texts[k2];
+            for (int u = threadIdx.x; u < t.w; u += kBlock) {
+                int i = 0;
+                while (i + 1 < t.len && t.start[i + 1] <= u) ++i;
+                colchar[k2][u] = (uint8_t)i;
             }
-            t.x0 = x0;
-            t.y0 = y0;
         }
         __syncthreads();
     }
@@ -260,6 +326,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     const int t0 = blockIdx.x * kBlock + threadIdx.x;
     if (t0 * kPix >= W * H) return;
     const int Y = (t0 * kPix) / W, X0 = (t0 * kPix) - Y * W;
+    const bool blk_bar = hud && row_lo < 30;  // the fuel bar's rows
     const int fuel_w = (int)(200.0 * (fuel / 1000.0));  // fuel_bar_width * fuel_percent
     const double fpct = fuel / 1000.0;
     const uint32_t fuel_color = fpct > 0.3 ? kGreen : fpct > 0.1 ? kYellow : kRed;
@@ -268,55 +335,49 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     for (int j = 0; j < kPix; ++j) {
         const int X = X0 + j;
         uint32_t col = Y >= p.ground ? kGround : kSky;
-        // Platform.render: fill, 2-px outline, centre line, "H"
-        if (X >= pl && X < pl + pw && Y >= pt && Y < pt + ph) {
-            const bool edge = X < pl + 2 || X >= pl + pw - 2 || Y < pt + 2 || Y >= pt + ph - 2;
-            col = edge ? kOutline : kPlatform;
-        }
-        if ((X == pcx || X == pcx + 1) && Y >= pt && Y <= pby) col = kWhite;
-        if (need_text) {
-            const int a = text_cover(texts[6], X, Y);
-            if (a) col = blend(col, texts[6].color, a);
-        }
-        // Drone.render: the sprite rotated about (x, y), nearest neighbour
-        const float dx = ((float)X + 0.5f) - xf, dy = ((float)Y + 0.5f) - yf;
-        if (fabsf(dx) <= hw + hh + 1.0f && fabsf(dy) <= hw + hh + 1.0f) {
-            const float u = dx * c + dy * s, w = dy * c - dx * s;
-            const float su = floorf(u + hw), sv = floorf(w + hh);
-            if (su >= 0.0f && su < (float)kDroneW && sv >= 0.0f && sv < 2.0f * hh) {
-                const int i = (int)su, k = (int)sv, cy = (int)hh;  // rotor / hub centres at height // 2
-                const int d0 = (i - kDroneW / 2) * (i - kDroneW / 2) + (k - cy) * (k - cy);
-                const int d1 = (i - 5) * (i - 5) + (k - cy) * (k - cy);
-                const int d2 = (i - (kDroneW - 5)) * (i - (kDroneW - 5)) + (k - cy) * (k - cy);
-                col = d0 <= 9 ? kHub : (d1 <= 25 || d2 <= 25) ? kRotor : kDrone;
+        if (blk_pad) {  // Platform.render: fill, 2-px outline, centre line, "H"
+            if (X >= pl && X < pl + pw && Y >= pt && Y < pt + ph) {
+                const bool edge = X < pl + 2 || X >= pl + pw - 2 || Y < pt + 2 || Y >= pt + ph - 2;
+                col = edge ? kOutline : kPlatform;
             }
+            if ((X == pcx || X == pcx + 1) && Y >= pt && Y <= pby) col = kWhite;
         }
-        // _render_thrust: main flame ellipse (fx - 8, fy - 7, 16, 15), side circles r = 5
-        if (main_on) {
-            const float ex = ((float)X + 0.5f - (float)mx) / 8.0f;
-            const float ey = ((float)Y + 0.5f - ((float)(my - 7) + 7.5f)) / 7.5f;
-            if (ex * ex + ey * ey <= 1.0f) col = kThrust;
+        if ((need >> 6) & 1u) col = draw_text(col, texts[6], colchar[6], fl, X, Y);
+        if (blk_drone) {
+            // Drone.render: the sprite rotated about (x, y), nearest neighbour
+            const float dx = ((float)X + 0.5f) - xf, dy = ((float)Y + 0.5f) - yf;
+            if (fabsf(dx) <= hw + hh + 1.0f && fabsf(dy) <= hw + hh + 1.0f) {
+                const float u = dx * c + dy * s, w = dy * c - dx * s;
+                const float su = floorf(u + hw), sv = floorf(w + hh);
+                if (su >= 0.0f && su < (float)kDroneW && sv >= 0.0f && sv < 2.0f * hh) {
+                    const int i = (int)su, k = (int)sv, cy = (int)hh;  // rotor / hub centres at height // 2
+                    const int d0 = (i - kDroneW / 2) * (i - kDroneW / 2) + (k - cy) * (k - cy);
+                    const int d1 = (i - 5) * (i - 5) + (k - cy) * (k - cy);
+                    const int d2 = (i - (kDroneW - 5)) * (i - (kDroneW - 5)) + (k - cy) * (k - cy);
+                    col = d0 <= 9 ? kHub : (d1 <= 25 || d2 <= 25) ? kRotor : kDrone;
+                }
+            }
+            // _render_thrust: main flame ellipse (fx - 8, fy - 7, 16, 15), side circles r = 5
+            if (main_on) {
+                const float ex = ((float)X + 0.5f - (float)mx) / 8.0f;
+                const float ey = ((float)Y + 0.5f - ((float)(my - 7) + 7.5f)) / 7.5f;
+                if (ex * ex + ey * ey <= 1.0f) col = kThrust;
+            }
+            if (left_on && (X - lx) * (X - lx) + (Y - ly) * (Y - ly) <= 25) col = kThrust;
+            if (right_on && (X - rx) * (X - rx) + (Y - ry) * (Y - ry) <= 25) col = kThrust;
         }
-        if (left_on && (X - lx) * (X - lx) + (Y - ly) * (Y - ly) <= 25) col = kThrust;
-        if (right_on && (X - rx) * (X - rx) + (Y - ry) * (Y - ry) <= 25) col = kThrust;
         // _render_hud
-        if (hud && Y < 130) {
-            if (X >= 10 && X < 210 && Y >= 10 && Y < 30) col = X < 10 + fuel_w ? fuel_color : kBarBg;
-#pragma unroll 1
-            for (int k = 0; k < 6; ++k) {
-                const int a = text_cover(texts[k], X, Y);
-                if (a) col = blend(col, texts[k].color, a);
-            }
+        if (blk_bar && X >= 10 && X < 210 && Y >= 10 && Y < 30) col = X < 10 + fuel_w ? fuel_color : kBarBg;
+        for (uint32_t m = need & 0x3Fu; m; m &= m - 1) {  // the HUD strings
+            const int k = __builtin_ctz(m);
+            col = draw_text(col, texts[k], colchar[k], fl, X, Y);
         }
         // _render_game_over
         if (over) {
             col = darken(col);
-            if (need_text) {
-#pragma unroll 1
-                for (int k = 7; k < kTexts; ++k) {
-                    const int a = text_cover(texts[k], X, Y);
-                    if (a) col = blend(col, texts[k].color, a);
-                }
+            for (uint32_t m = need & 0x380u; m; m &= m - 1) {
+                const int k = __builtin_ctz(m);
+                col = draw_text(col, texts[k], colchar[k], fl, X, Y);
             }
         }
         px4[j] = col;
@@ -348,9 +409,9 @@ inline bool whole(double d, double lo, double hi) { return d >= lo && d <= hi &&
 }  // namespace dd
 
 extern "C" int dd_render(const DDConfig* cfg, const DDState* st, const uint8_t* actions, const int32_t* lanes,
-                         int64_t count, uint8_t* rgb, int32_t flags, void* stream) {
+                         int64_t count, int64_t n, uint8_t* rgb, int32_t flags, void* stream) {
     using namespace dd::render;
-    if (!cfg || !st || count < 0) return (int)hipErrorInvalidValue;
+    if (!cfg || !st || count < 0 || n < 0 || (!lanes && count > n)) return (int)hipErrorInvalidValue;
     if (count == 0) return 0;
     if (!rgb || !st->x || !st->y || !st->vx || !st->vy || !st->angle || !st->fuel || !st->px || !st->py ||
         !st->total_reward || !st->status || !st->steps || !st->episode)
@@ -368,6 +429,7 @@ extern "C" int dd_render(const DDConfig* cfg, const DDState* st, const uint8_t* 
     p.height = (int32_t)cfg->world_height;
     p.ground = (int32_t)cfg->ground_level;
     p.count = (int32_t)count;
+    p.n = n;
     p.phw = (int32_t)cfg->platform_half_width;
     p.phh = (int32_t)cfg->platform_half_height;
     p.dhh = (int32_t)cfg->drone_half_height;

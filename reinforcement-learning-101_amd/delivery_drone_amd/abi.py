@@ -129,7 +129,8 @@ EXPORTS = {
     "dd_mlp_forward": (ctypes.c_int, [ctypes.c_void_p, _I, ctypes.POINTER(DDMlpIO), ctypes.c_int64,
                                       ctypes.c_void_p]),
     "dd_render": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
-                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, _I, ctypes.c_void_p]),
+                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, _I,
+                                 ctypes.c_void_p]),
     "dd_step_bytes_per_env": (ctypes.c_int64, [_I, _I, _I]),
     "dd_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dd_abi_version": (ctypes.c_int, []),

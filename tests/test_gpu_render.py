@@ -86,6 +86,9 @@ def test_render_lanes_flags_and_remembered_actions(gpu_device):
     assert np.array_equal(frame, R.render(lane_values(env, 3), 0))
     with pytest.raises(IndexError):
         env.render(lanes=[n])
+    frames = env.render(lanes=torch.tensor([n, 1, -1], device=gpu_device)).cpu().numpy()
+    assert not frames[0].any() and not frames[2].any()  # not a lane: all zero
+    assert np.array_equal(frames[1], R.render(lane_values(env, 1), 0))
 
 
 def test_dronegame_rgb_array(gpu_device):

@@ -1,0 +1,50 @@
+#!/usr/bin/env python
+"""Timing of dd_render: `frames` lanes of a running 4,096-lane batch per launch
+(HUD on or off; lanes that are done get the game-over overlay).  20 launches
+captured in a hipGraph, replayed and timed with HIP events, so the number is
+device time, not the Python wrapper's."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
+import torch  # noqa: E402
+from delivery_drone_amd import EnvConfig, VecDroneEnv  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    env = VecDroneEnv(4096, device=dev, config=EnvConfig(randomize_drone=True, auto_reset=False, seed=0))
+    env.reset()
+    acts = torch.randint(0, 8, (4096,), device=dev, dtype=torch.uint8)
+    for _ in range(60):
+        env.step(acts)
+    stream = torch.cuda.Stream(dev)
+    for frames in (1, 16, 64, 256):
+        lanes = torch.arange(0, 4096, 4096 // frames, dtype=torch.int32, device=dev)[:frames]
+        out = torch.empty(frames, 600, 800, 3, dtype=torch.uint8, device=dev)
+        for hud in (True, False):
+            with torch.cuda.stream(stream):
+                env.render(lanes=lanes, out=out, hud=hud, actions=acts)
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                reps = 20
+                with torch.cuda.graph(g, stream=stream):
+                    for _ in range(reps):
+                        env.render(lanes=lanes, out=out, hud=hud, actions=acts)
+                g.replay()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                g.replay()
+                e1.record(stream)
+                torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            gbs = frames * 1.44e6 / (us * 1e-6) / 1e9
+            print(json.dumps({"frames": frames, "hud": hud, "us": round(us, 2), "frames_per_s": round(frames / us * 1e6),
+                              "gbs": round(gbs, 1), "done_lanes": int(env.done[lanes.long()].sum())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
