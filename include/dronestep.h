@@ -303,7 +303,8 @@ enum { DD_RENDER_HUD = 1, DD_RENDER_GAME_OVER = 2 };
  * 0..count-1 (count <= n); a frame whose index is outside [0, n) is left
  * all zero.  actions (nullable): the uint8 [n] bitmask of the last step, which
  * _render_thrust draws as flames (drone.py:189-218, where fuel > 0); NULL
- * draws none, as after a reset.  flags: DD_RENDER_*. */
+ * draws none, and so does a lane whose steps is 0 (Drone.reset clears the
+ * thrusters).  flags: DD_RENDER_*. */
 int dd_render(const DDConfig *cfg, const DDState *st, const uint8_t *actions,
               const int32_t *lanes, int64_t count, int64_t n, uint8_t *rgb,
               int32_t flags, void *stream);

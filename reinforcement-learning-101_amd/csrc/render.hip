@@ -42,7 +42,8 @@ namespace dd {
 namespace render {
 
 constexpr int kBlock = 256;
-constexpr int kPix = 4;  // pixels per lane
+constexpr int kPix = 4;    // consecutive pixels per lane and pass (12 output bytes)
+constexpr int kQuads = 8;  // passes per lane: a block covers kBlock * kPix * kQuads = 8,192 pixels
 constexpr int kTexts = 10;
 constexpr int kMaxChars = 32;
 constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
@@ -180,12 +181,14 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     const int slot = blockIdx.y;
     const int lane = p.lanes ? p.lanes[slot] : slot;
     if (lane < 0 || lane >= p.n) {  // not a lane: an all-zero frame
-        const int t = blockIdx.x * kBlock + threadIdx.x;
-        if (t * kPix < p.width * p.height) {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(p.rgb + ((size_t)slot * p.width * p.height + (size_t)t * kPix) * 3);
-            __builtin_nontemporal_store(0u, dst);
-            __builtin_nontemporal_store(0u, dst + 1);
-            __builtin_nontemporal_store(0u, dst + 2);
+        for (int q = 0; q < kQuads; ++q) {
+            const int t = (blockIdx.x * kQuads + q) * kBlock + threadIdx.x;
+            if (t * kPix < p.width * p.height) {
+                uint32_t* dst = reinterpret_cast<uint32_t*>(p.rgb + ((size_t)slot * p.width * p.height + (size_t)t * kPix) * 3);
+                __builtin_nontemporal_store(0u, dst);
+                __builtin_nontemporal_store(0u, dst + 1);
+                __builtin_nontemporal_store(0u, dst + 2);
+            }
         }
         return;
     }
@@ -193,10 +196,11 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     const double x = (double)v.x[lane], y = (double)v.y[lane], angle = (double)v.angle[lane];
     const double fuel = (double)v.fuel[lane], px = (double)v.px[lane], py = (double)v.py[lane];
     const uint32_t status = v.status[lane];
-    const uint32_t act = p.actions ? p.actions[lane] : 0u;
+    // flames: the last step's thrusters; none on a fresh episode (Drone.reset clears them)
+    const uint32_t act = (p.actions && v.steps[lane] > 0) ? (p.actions[lane] & 7u) : 0u;
     const int W = p.width, H = p.height;
-    const int first = (blockIdx.x * kBlock) * kPix;  // this block's first pixel
-    const int row_lo = first / W, row_hi = min(H - 1, (first + kBlock * kPix - 1) / W);
+    const int first = blockIdx.x * kBlock * kPix * kQuads;  // this block's first pixel
+    const int row_lo = first / W, row_hi = min(H - 1, (first + kBlock * kPix * kQuads - 1) / W);
 
     // float32 geometry of the rotated parts (see the header)
     double sd, cd;
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     const bool hud = p.flags & DD_RENDER_HUD;
     const bool over = (p.flags & DD_RENDER_GAME_OVER) && (status & DD_ST_DONE);
 
-    // Block culling: a block covers kBlock * kPix = 1,024 pixels (1-2 rows),
+    // Block culling: a block covers 8,192 consecutive pixels (11-12 rows),
     // so each group of primitives is tested against the block's rows once
     // (a scalar branch) and most blocks only fill sky or ground.
     //   pad band: the platform and its centre line (pt .. bottom);
@@ -323,73 +327,75 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
         __syncthreads();
     }
 
-    const int t0 = blockIdx.x * kBlock + threadIdx.x;
-    if (t0 * kPix >= W * H) return;
-    const int Y = (t0 * kPix) / W, X0 = (t0 * kPix) - Y * W;
     const bool blk_bar = hud && row_lo < 30;  // the fuel bar's rows
     const int fuel_w = (int)(200.0 * (fuel / 1000.0));  // fuel_bar_width * fuel_percent
     const double fpct = fuel / 1000.0;
     const uint32_t fuel_color = fpct > 0.3 ? kGreen : fpct > 0.1 ? kYellow : kRed;
-    uint32_t px4[kPix];
+    for (int q = 0; q < kQuads; ++q) {  // pass q: the block's q-th run of kBlock * kPix pixels
+        const int t0 = (blockIdx.x * kQuads + q) * kBlock + threadIdx.x;
+        if (t0 * kPix >= W * H) break;
+        const int Y = (t0 * kPix) / W, X0 = (t0 * kPix) - Y * W;
+        uint32_t px4[kPix];
 #pragma unroll
-    for (int j = 0; j < kPix; ++j) {
-        const int X = X0 + j;
-        uint32_t col = Y >= p.ground ? kGround : kSky;
-        if (blk_pad) {  // Platform.render: fill, 2-px outline, centre line, "H"
-            if (X >= pl && X < pl + pw && Y >= pt && Y < pt + ph) {
-                const bool edge = X < pl + 2 || X >= pl + pw - 2 || Y < pt + 2 || Y >= pt + ph - 2;
-                col = edge ? kOutline : kPlatform;
-            }
-            if ((X == pcx || X == pcx + 1) && Y >= pt && Y <= pby) col = kWhite;
-        }
-        if ((need >> 6) & 1u) col = draw_text(col, texts[6], colchar[6], fl, X, Y);
-        if (blk_drone) {
-            // Drone.render: the sprite rotated about (x, y), nearest neighbour
-            const float dx = ((float)X + 0.5f) - xf, dy = ((float)Y + 0.5f) - yf;
-            if (fabsf(dx) <= hw + hh + 1.0f && fabsf(dy) <= hw + hh + 1.0f) {
-                const float u = dx * c + dy * s, w = dy * c - dx * s;
-                const float su = floorf(u + hw), sv = floorf(w + hh);
-                if (su >= 0.0f && su < (float)kDroneW && sv >= 0.0f && sv < 2.0f * hh) {
-                    const int i = (int)su, k = (int)sv, cy = (int)hh;  // rotor / hub centres at height // 2
-                    const int d0 = (i - kDroneW / 2) * (i - kDroneW / 2) + (k - cy) * (k - cy);
-                    const int d1 = (i - 5) * (i - 5) + (k - cy) * (k - cy);
-                    const int d2 = (i - (kDroneW - 5)) * (i - (kDroneW - 5)) + (k - cy) * (k - cy);
-                    col = d0 <= 9 ? kHub : (d1 <= 25 || d2 <= 25) ? kRotor : kDrone;
+        for (int j = 0; j < kPix; ++j) {
+            const int X = X0 + j;
+            uint32_t col = Y >= p.ground ? kGround : kSky;
+            if (blk_pad) {  // Platform.render: fill, 2-px outline, centre line, "H"
+                if (X >= pl && X < pl + pw && Y >= pt && Y < pt + ph) {
+                    const bool edge = X < pl + 2 || X >= pl + pw - 2 || Y < pt + 2 || Y >= pt + ph - 2;
+                    col = edge ? kOutline : kPlatform;
                 }
+                if ((X == pcx || X == pcx + 1) && Y >= pt && Y <= pby) col = kWhite;
             }
-            // _render_thrust: main flame ellipse (fx - 8, fy - 7, 16, 15), side circles r = 5
-            if (main_on) {
-                const float ex = ((float)X + 0.5f - (float)mx) / 8.0f;
-                const float ey = ((float)Y + 0.5f - ((float)(my - 7) + 7.5f)) / 7.5f;
-                if (ex * ex + ey * ey <= 1.0f) col = kThrust;
+            if ((need >> 6) & 1u) col = draw_text(col, texts[6], colchar[6], fl, X, Y);
+            if (blk_drone) {
+                // Drone.render: the sprite rotated about (x, y), nearest neighbour
+                const float dx = ((float)X + 0.5f) - xf, dy = ((float)Y + 0.5f) - yf;
+                if (fabsf(dx) <= hw + hh + 1.0f && fabsf(dy) <= hw + hh + 1.0f) {
+                    const float u = dx * c + dy * s, w = dy * c - dx * s;
+                    const float su = floorf(u + hw), sv = floorf(w + hh);
+                    if (su >= 0.0f && su < (float)kDroneW && sv >= 0.0f && sv < 2.0f * hh) {
+                        const int i = (int)su, k = (int)sv, cy = (int)hh;  // rotor / hub centres at height // 2
+                        const int d0 = (i - kDroneW / 2) * (i - kDroneW / 2) + (k - cy) * (k - cy);
+                        const int d1 = (i - 5) * (i - 5) + (k - cy) * (k - cy);
+                        const int d2 = (i - (kDroneW - 5)) * (i - (kDroneW - 5)) + (k - cy) * (k - cy);
+                        col = d0 <= 9 ? kHub : (d1 <= 25 || d2 <= 25) ? kRotor : kDrone;
+                    }
+                }
+                // _render_thrust: main flame ellipse (fx - 8, fy - 7, 16, 15), side circles r = 5
+                if (main_on) {
+                    const float ex = ((float)X + 0.5f - (float)mx) / 8.0f;
+                    const float ey = ((float)Y + 0.5f - ((float)(my - 7) + 7.5f)) / 7.5f;
+                    if (ex * ex + ey * ey <= 1.0f) col = kThrust;
+                }
+                if (left_on && (X - lx) * (X - lx) + (Y - ly) * (Y - ly) <= 25) col = kThrust;
+                if (right_on && (X - rx) * (X - rx) + (Y - ry) * (Y - ry) <= 25) col = kThrust;
             }
-            if (left_on && (X - lx) * (X - lx) + (Y - ly) * (Y - ly) <= 25) col = kThrust;
-            if (right_on && (X - rx) * (X - rx) + (Y - ry) * (Y - ry) <= 25) col = kThrust;
-        }
-        // _render_hud
-        if (blk_bar && X >= 10 && X < 210 && Y >= 10 && Y < 30) col = X < 10 + fuel_w ? fuel_color : kBarBg;
-        for (uint32_t m = need & 0x3Fu; m; m &= m - 1) {  // the HUD strings
-            const int k = __builtin_ctz(m);
-            col = draw_text(col, texts[k], colchar[k], fl, X, Y);
-        }
-        // _render_game_over
-        if (over) {
-            col = darken(col);
-            for (uint32_t m = need & 0x380u; m; m &= m - 1) {
+            // _render_hud
+            if (blk_bar && X >= 10 && X < 210 && Y >= 10 && Y < 30) col = X < 10 + fuel_w ? fuel_color : kBarBg;
+            for (uint32_t m = need & 0x3Fu; m; m &= m - 1) {  // the HUD strings
                 const int k = __builtin_ctz(m);
                 col = draw_text(col, texts[k], colchar[k], fl, X, Y);
             }
+            // _render_game_over
+            if (over) {
+                col = darken(col);
+                for (uint32_t m = need & 0x380u; m; m &= m - 1) {
+                    const int k = __builtin_ctz(m);
+                    col = draw_text(col, texts[k], colchar[k], fl, X, Y);
+                }
+            }
+            px4[j] = col;
         }
-        px4[j] = col;
+        // 4 RGB pixels = 3 dwords, little-endian byte order R G B R G B ...
+        const uint32_t w0 = (px4[0] & 0xFFFFFFu) | (px4[1] << 24);
+        const uint32_t w1 = ((px4[1] >> 8) & 0xFFFFu) | (px4[2] << 16);
+        const uint32_t w2 = ((px4[2] >> 16) & 0xFFu) | (px4[3] << 8);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(p.rgb + ((size_t)slot * W * H + (size_t)t0 * kPix) * 3);
+        __builtin_nontemporal_store(w0, dst);
+        __builtin_nontemporal_store(w1, dst + 1);
+        __builtin_nontemporal_store(w2, dst + 2);
     }
-    // 4 RGB pixels = 3 dwords, little-endian byte order R G B R G B ...
-    const uint32_t w0 = (px4[0] & 0xFFFFFFu) | (px4[1] << 24);
-    const uint32_t w1 = ((px4[1] >> 8) & 0xFFFFu) | (px4[2] << 16);
-    const uint32_t w2 = ((px4[2] >> 16) & 0xFFu) | (px4[3] << 8);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(p.rgb + ((size_t)slot * W * H + (size_t)t0 * kPix) * 3);
-    __builtin_nontemporal_store(w0, dst);
-    __builtin_nontemporal_store(w1, dst + 1);
-    __builtin_nontemporal_store(w2, dst + 2);
 }
 
 template <typename T>
@@ -434,7 +440,7 @@ extern "C" int dd_render(const DDConfig* cfg, const DDState* st, const uint8_t* 
     p.phh = (int32_t)cfg->platform_half_height;
     p.dhh = (int32_t)cfg->drone_half_height;
     p.flags = flags;
-    const int64_t quads = (int64_t)p.width * p.height / kPix;
+    const int64_t quads = ((int64_t)p.width * p.height / kPix + kQuads - 1) / kQuads;
     dim3 grid((unsigned)((quads + kBlock - 1) / kBlock), (unsigned)count);
     hipStream_t s = (hipStream_t)stream;
     if (st->precision == DD_F64)
