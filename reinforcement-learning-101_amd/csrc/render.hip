@@ -60,13 +60,25 @@ constexpr int kDroneW = 40;  // config.DRONE_WIDTH (the sprite; the physics neve
 // One string of the frame, laid out: its chars, the glyph and left edge of
 // each, and (built per block) the char under every column of its box.
 constexpr int kMaxTextW = 640;
+// The fixed text of each string (index 10: the title of a crash).
+__device__ constexpr char kPrefix[11][20] = {"Fuel: ", "Speed: ", "Angle: ", "Distance: ", "Episode: ",
+                                             "Steps: ", "H", "SUCCESSFUL LANDING!", "Total Reward: ",
+                                             "Press R to restart", "CRASHED!"};
+
 struct Text {
     int32_t x0, y0, w, h, face, len;
     uint32_t color;
     uint8_t s[kMaxChars];
     int16_t glyph[kMaxChars];
     int16_t start[kMaxChars];
+    int32_t r0, roff;  // this block's first row of it, and where those rows sit in the raster (-1: not staged)
 };
+
+// Per block, the coverage of the rows of each drawn string that fall in the
+// block's rows, staged in LDS once, so a text pixel is one LDS read: read
+// straight from the atlas in global memory, a HUD block waited on a chain of
+// dependent loads per pass (strings x pixels x passes).
+constexpr int kRaster = 16384;
 
 // ---- f-string formatting (Python's int() / str(int) / format(x, '.Nf')) ----
 struct Str {
@@ -123,16 +135,9 @@ __device__ __forceinline__ uint32_t blend(uint32_t d, uint32_t s, int a) {
     return out;
 }
 
-// the game-over overlay: black at surface alpha 128
-__device__ __forceinline__ uint32_t darken(uint32_t d) {
-    uint32_t out = 0;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        const int dc = (int)((d >> (8 * ch)) & 255u);
-        out |= (uint32_t)(dc + ((-dc * 128) >> 8)) << (8 * ch);
-    }
-    return out;
-}
+// the game-over overlay, black at surface alpha 128: d + ((-d * 128) >> 8)
+// = d - ceil(d / 2) = floor(d / 2) per channel, i.e. every byte halved
+__device__ __forceinline__ uint32_t darken(uint32_t d) { return (d >> 1) & 0x7F7F7Fu; }
 
 // The font tables a block reads while laying out and drawing its strings,
 // copied to LDS once (the layout walks them char by char: from global
@@ -146,14 +151,32 @@ struct FontLds {
 // string t blended over colour d at pixel (X, Y) (pygame ALPHA_BLEND of the
 // glyph's coverage); d unchanged outside its box
 __device__ __forceinline__ uint32_t draw_text(uint32_t d, const Text& t, const uint8_t* cc, const FontLds& fl,
-                                              int X, int Y) {
+                                              const uint8_t* raster, int X, int Y) {
     const int u = X - t.x0, v = Y - t.y0;
     if (u < 0 || u >= t.w || v < 0 || v >= t.h || t.len == 0) return d;
-    const int i = cc[u];
-    const int g = t.glyph[i];
-    const int adv = fl.advance[g];
-    const int a = font::kAtlas[fl.offset[g] + v * adv + (u - t.start[i])];
+    int a;
+    if (t.roff >= 0) {
+        a = raster[t.roff + (Y - t.r0) * t.w + u];
+    } else {  // did not fit the raster: from the atlas
+        const int i = cc[u];
+        const int g = t.glyph[i];
+        a = font::kAtlas[fl.offset[g] + v * fl.advance[g] + (u - t.start[i])];
+    }
     return a ? blend(d, t.color, a) : d;
+}
+
+// the strings of `mask` over a lane's 4 pixels (X0 .. X0 + 3, row Y), each
+// only where its rows and columns meet them
+__device__ __forceinline__ void draw_texts(uint32_t (&px4)[kPix], uint32_t mask, const Text* texts,
+                                           const uint8_t (*colchar)[kMaxTextW], const FontLds& fl,
+                                           const uint8_t* raster, int X0, int Y) {
+    for (uint32_t m = mask; m; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        const Text& t = texts[k];
+        if (Y < t.y0 || Y >= t.y0 + t.h || X0 + kPix <= t.x0 || X0 >= t.x0 + t.w) continue;
+#pragma unroll
+        for (int j = 0; j < kPix; ++j) px4[j] = draw_text(px4[j], t, colchar[k], fl, raster, X0 + j, Y);
+    }
 }
 
 struct Args {
@@ -177,6 +200,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
     __shared__ Text texts[kTexts];
     __shared__ uint8_t colchar[kTexts][kMaxTextW];
+    __shared__ uint8_t raster[kRaster];
     __shared__ FontLds fl;
     const int slot = blockIdx.y;
     const int lane = p.lanes ? p.lanes[slot] : slot;
@@ -265,35 +289,32 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
         if (k < kTexts && ((need >> k) & 1u)) {
             Text& t = texts[k];
             Str str{t.s, 0};
-            uint32_t color = kWhite;
-            switch (k) {
-                case 0:  // f"Fuel: {int(self.drone.fuel)}" at (15, 12)
-                    str.put("Fuel: "); str.put_i64((int64_t)fuel); break;
-                case 1: {  // f"Speed: {get_speed():.1f}" at (10, 40)
-                    const double vx = (double)v.vx[lane], vy = (double)v.vy[lane];
-                    str.put("Speed: "); str.put_fixed(sqrt(vx * vx + vy * vy), 1); break;
-                }
-                case 2:  // f"Angle: {angle:.1f}°" at (10, 65)
-                    str.put("Angle: "); str.put_fixed(angle, 1); str.put((char)font::kDegree); break;
-                case 3: {  // f"Distance: {distance:.0f}" at (10, 90)
-                    const double dx = px - x, dy = py - y;
-                    str.put("Distance: "); str.put_fixed(sqrt(dx * dx + dy * dy), 0); break;
-                }
-                case 4:  // f"Episode: {episode}" at (W - 150, 10)
-                    str.put("Episode: "); str.put_i64(v.episode[lane]); break;
-                case 5:  // f"Steps: {steps}" at (W - 150, 35)
-                    str.put("Steps: "); str.put_i64(v.steps[lane]); break;
-                case 6:  // the pad's "H", centred on (int(x), int(y))
-                    str.put("H"); break;
-                case 7:  // game-over title, centred on (W // 2, H // 2 - 30)
-                    if (status & DD_ST_LANDED) { str.put("SUCCESSFUL LANDING!"); color = kGreen; }
-                    else { str.put("CRASHED!"); color = kRed; }
-                    break;
-                case 8:  // f"Total Reward: {total_reward:.1f}", centred on (W // 2, H // 2 + 20)
-                    str.put("Total Reward: "); str.put_fixed((double)v.total[lane], 1); break;
-                default:  // "Press R to restart", centred on (W // 2, H // 2 + 50)
-                    str.put("Press R to restart"); break;
+            // One code path for all ten strings (they are laid out by ten lanes
+            // of one wave): prefix from a table, then at most one number.
+            //   0 f"Fuel: {int(fuel)}"      (15, 12)   5 f"Steps: {steps}"     (W - 150, 35)
+            //   1 f"Speed: {speed:.1f}"     (10, 40)   6 "H", centred on the pad
+            //   2 f"Angle: {angle:.1f}°"    (10, 65)   7 game-over title, (W // 2, H // 2 - 30)
+            //   3 f"Distance: {dist:.0f}"   (10, 90)   8 f"Total Reward: {total:.1f}" (W // 2, H // 2 + 20)
+            //   4 f"Episode: {episode}"     (W - 150, 10)  9 "Press R to restart" (W // 2, H // 2 + 50)
+            const double vx = (double)v.vx[lane], vy = (double)v.vy[lane], dx = px - x, dy = py - y;
+            const bool landed = (status & DD_ST_LANDED) != 0;
+            const int pre = k == 7 ? (landed ? 7 : 10) : k;
+            double num = 0.0;
+            int decimals = -1;  // -1: no number; 0: integer or .0f; 1: .1f
+            switch (k) {  // selects only: every lane runs the same instructions
+                case 0: num = (double)(int64_t)fuel; decimals = 0; break;
+                case 1: num = sqrt(vx * vx + vy * vy); decimals = 1; break;
+                case 2: num = angle; decimals = 1; break;
+                case 3: num = sqrt(dx * dx + dy * dy); decimals = 0; break;
+                case 4: num = (double)v.episode[lane]; decimals = 0; break;
+                case 5: num = (double)v.steps[lane]; decimals = 0; break;
+                case 8: num = (double)v.total[lane]; decimals = 1; break;
+                default: break;
             }
+            for (const char* c = kPrefix[pre]; *c; ++c) str.put(*c);
+            if (decimals >= 0) str.put_fixed(num, decimals);
+            if (k == 2) str.put((char)font::kDegree);
+            const uint32_t color = k != 7 ? kWhite : landed ? kGreen : kRed;
             const int face = tface[k];
             int w = 0, n = 0;
             for (int i = 0; i < str.n; ++i) {  // glyphs with a cell in this face, side by side
@@ -314,6 +335,16 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
             t.y0 = tcentre[k] ? ty[k] - t.h / 2 : ty[k];
         }
         __syncthreads();
+        if (threadIdx.x == 0) {  // raster slots for the block's rows of each string
+            int off = 0;
+            for (uint32_t m = need; m; m &= m - 1) {
+                Text& t = texts[__builtin_ctz(m)];
+                t.r0 = max(t.y0, row_lo);
+                const int bytes = max(0, min(t.y0 + t.h, row_hi + 1) - t.r0) * t.w;
+                t.roff = off + bytes <= kRaster ? off : -1;
+                if (t.roff >= 0) off += bytes;
+            }
+        }
         // the char under every column of each string drawn here
         for (uint32_t m = need; m; m &= m - 1) {
             const int k2 = __builtin_ctz(m);
@@ -322,6 +353,19 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
                 int i = 0;
                 while (i + 1 < t.len && t.start[i + 1] <= u) ++i;
                 colchar[k2][u] = (uint8_t)i;
+            }
+        }
+        __syncthreads();
+        for (uint32_t m = need; m; m &= m - 1) {  // stage the coverage: independent loads, all lanes
+            const int k2 = __builtin_ctz(m);
+            const Text& t = texts[k2];
+            if (t.roff < 0 || t.w == 0) continue;
+            const int bytes = max(0, min(t.y0 + t.h, row_hi + 1) - t.r0) * t.w;
+            for (int e = threadIdx.x; e < bytes; e += kBlock) {
+                const int row = e / t.w, u = e - row * t.w;
+                const int i = colchar[k2][u];
+                const int g = t.glyph[i];
+                raster[t.roff + e] = font::kAtlas[fl.offset[g] + (t.r0 + row - t.y0) * fl.advance[g] + (u - t.start[i])];
             }
         }
         __syncthreads();
@@ -335,23 +379,30 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
         const int t0 = (blockIdx.x * kQuads + q) * kBlock + threadIdx.x;
         if (t0 * kPix >= W * H) break;
         const int Y = (t0 * kPix) / W, X0 = (t0 * kPix) - Y * W;
-        uint32_t px4[kPix];
+        // Each primitive is gated by the pass's row first (the lane's 4 pixels
+        // share Y, and a wave's 256 pixels span one or two rows), so a pass
+        // through sky or ground costs a handful of instructions.
+        const uint32_t base = Y >= p.ground ? kGround : kSky;
+        uint32_t px4[kPix] = {base, base, base, base};
+        if (blk_pad && Y >= pt && Y <= pby) {  // Platform.render: fill, 2-px outline, centre line
 #pragma unroll
-        for (int j = 0; j < kPix; ++j) {
-            const int X = X0 + j;
-            uint32_t col = Y >= p.ground ? kGround : kSky;
-            if (blk_pad) {  // Platform.render: fill, 2-px outline, centre line, "H"
-                if (X >= pl && X < pl + pw && Y >= pt && Y < pt + ph) {
+            for (int j = 0; j < kPix; ++j) {
+                const int X = X0 + j;
+                if (X >= pl && X < pl + pw && Y < pt + ph) {
                     const bool edge = X < pl + 2 || X >= pl + pw - 2 || Y < pt + 2 || Y >= pt + ph - 2;
-                    col = edge ? kOutline : kPlatform;
+                    px4[j] = edge ? kOutline : kPlatform;
                 }
-                if ((X == pcx || X == pcx + 1) && Y >= pt && Y <= pby) col = kWhite;
+                if (X == pcx || X == pcx + 1) px4[j] = kWhite;
             }
-            if ((need >> 6) & 1u) col = draw_text(col, texts[6], colchar[6], fl, X, Y);
-            if (blk_drone) {
+        }
+        draw_texts(px4, need & 0x40u, texts, colchar, fl, raster, X0, Y);  // the pad's "H"
+        if (blk_drone && fabsf(((float)Y + 0.5f) - yf) <= hw + hh + 1.0f) {
+#pragma unroll
+            for (int j = 0; j < kPix; ++j) {
+                const int X = X0 + j;
                 // Drone.render: the sprite rotated about (x, y), nearest neighbour
                 const float dx = ((float)X + 0.5f) - xf, dy = ((float)Y + 0.5f) - yf;
-                if (fabsf(dx) <= hw + hh + 1.0f && fabsf(dy) <= hw + hh + 1.0f) {
+                if (fabsf(dx) <= hw + hh + 1.0f) {
                     const float u = dx * c + dy * s, w = dy * c - dx * s;
                     const float su = floorf(u + hw), sv = floorf(w + hh);
                     if (su >= 0.0f && su < (float)kDroneW && sv >= 0.0f && sv < 2.0f * hh) {
@@ -359,33 +410,33 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
                         const int d0 = (i - kDroneW / 2) * (i - kDroneW / 2) + (k - cy) * (k - cy);
                         const int d1 = (i - 5) * (i - 5) + (k - cy) * (k - cy);
                         const int d2 = (i - (kDroneW - 5)) * (i - (kDroneW - 5)) + (k - cy) * (k - cy);
-                        col = d0 <= 9 ? kHub : (d1 <= 25 || d2 <= 25) ? kRotor : kDrone;
+                        px4[j] = d0 <= 9 ? kHub : (d1 <= 25 || d2 <= 25) ? kRotor : kDrone;
                     }
                 }
                 // _render_thrust: main flame ellipse (fx - 8, fy - 7, 16, 15), side circles r = 5
                 if (main_on) {
                     const float ex = ((float)X + 0.5f - (float)mx) / 8.0f;
                     const float ey = ((float)Y + 0.5f - ((float)(my - 7) + 7.5f)) / 7.5f;
-                    if (ex * ex + ey * ey <= 1.0f) col = kThrust;
+                    if (ex * ex + ey * ey <= 1.0f) px4[j] = kThrust;
                 }
-                if (left_on && (X - lx) * (X - lx) + (Y - ly) * (Y - ly) <= 25) col = kThrust;
-                if (right_on && (X - rx) * (X - rx) + (Y - ry) * (Y - ry) <= 25) col = kThrust;
+                if (left_on && (X - lx) * (X - lx) + (Y - ly) * (Y - ly) <= 25) px4[j] = kThrust;
+                if (right_on && (X - rx) * (X - rx) + (Y - ry) * (Y - ry) <= 25) px4[j] = kThrust;
             }
-            // _render_hud
-            if (blk_bar && X >= 10 && X < 210 && Y >= 10 && Y < 30) col = X < 10 + fuel_w ? fuel_color : kBarBg;
-            for (uint32_t m = need & 0x3Fu; m; m &= m - 1) {  // the HUD strings
-                const int k = __builtin_ctz(m);
-                col = draw_text(col, texts[k], colchar[k], fl, X, Y);
+        }
+        // _render_hud
+        if (blk_bar && Y >= 10 && Y < 30) {
+#pragma unroll
+            for (int j = 0; j < kPix; ++j) {
+                const int X = X0 + j;
+                if (X >= 10 && X < 210) px4[j] = X < 10 + fuel_w ? fuel_color : kBarBg;
             }
-            // _render_game_over
-            if (over) {
-                col = darken(col);
-                for (uint32_t m = need & 0x380u; m; m &= m - 1) {
-                    const int k = __builtin_ctz(m);
-                    col = draw_text(col, texts[k], colchar[k], fl, X, Y);
-                }
-            }
-            px4[j] = col;
+        }
+        draw_texts(px4, need & 0x3Fu, texts, colchar, fl, raster, X0, Y);
+        // _render_game_over
+        if (over) {
+#pragma unroll
+            for (int j = 0; j < kPix; ++j) px4[j] = darken(px4[j]);
+            draw_texts(px4, need & 0x380u, texts, colchar, fl, raster, X0, Y);
         }
         // 4 RGB pixels = 3 dwords, little-endian byte order R G B R G B ...
         const uint32_t w0 = (px4[0] & 0xFFFFFFu) | (px4[1] << 24);
