@@ -360,12 +360,12 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
             const int k2 = __builtin_ctz(m);
             const Text& t = texts[k2];
             if (t.roff < 0 || t.w == 0) continue;
-            const int bytes = max(0, min(t.y0 + t.h, row_hi + 1) - t.r0) * t.w;
-            for (int e = threadIdx.x; e < bytes; e += kBlock) {
-                const int row = e / t.w, u = e - row * t.w;
+            const int rows = max(0, min(t.y0 + t.h, row_hi + 1) - t.r0);
+            for (int u = threadIdx.x; u < t.w; u += kBlock) {  // a column per lane, its rows in turn
                 const int i = colchar[k2][u];
-                const int g = t.glyph[i];
-                raster[t.roff + e] = font::kAtlas[fl.offset[g] + (t.r0 + row - t.y0) * fl.advance[g] + (u - t.start[i])];
+                const int adv = fl.advance[t.glyph[i]];
+                const uint8_t* src = font::kAtlas + fl.offset[t.glyph[i]] + (t.r0 - t.y0) * adv + (u - t.start[i]);
+                for (int r = 0; r < rows; ++r) raster[t.roff + r * t.w + u] = src[r * adv];
             }
         }
         __syncthreads();
