@@ -117,6 +117,27 @@ def test_argument_errors_return_invalid_value_without_gpu():
     assert lib.dd_error_string(EINVAL)
 
 
+def test_render_argument_errors_without_gpu():
+    lib = abi.lib()
+    cfg = EnvConfig().to_abi()
+    EINVAL = 1
+    st, rgb = _state(), ctypes.c_void_p(8)
+
+    def render(c=cfg, state=st, lanes=None, count=2, n=4, out=rgb, flags=3):
+        return lib.dd_render(ctypes.byref(c) if c is not None else None, ctypes.byref(state), None, lanes, count, n,
+                             out, flags, None)
+
+    assert render(c=None) == EINVAL
+    assert render(count=-1) == EINVAL
+    assert render(n=-1) == EINVAL
+    assert render(count=5, n=4) == EINVAL  # lanes 0..4 of a 4-lane batch
+    assert render(out=None) == EINVAL
+    assert render(state=abi.DDState()) == EINVAL  # null SoA pointers
+    assert render(state=_state(precision=7)) == EINVAL
+    assert render(c=EnvConfig(world_width=802).to_abi()) == EINVAL  # rows are drawn 4 pixels at a time
+    assert render(count=0) == 0  # nothing to draw
+
+
 def test_byte_model():
     lib = abi.lib()
     # f32, bitmask actions, obs: reads 10*4+1+4+1, writes 9*4+4+1, obs 60
