@@ -98,9 +98,6 @@ struct Str {
         do { tmp[k++] = (char)('0' + w % 10u); w /= 10u; } while (w);
         while (k) put(tmp[--k]);
     }
-    __device__ void put_i64(int64_t v) {
-        if (v < 0) { put('-'); put_u64((uint64_t)(-(v + 1)) + 1u); } else { put_u64((uint64_t)v); }
-    }
     // format(x, '.1f') / '.0f': the correctly rounded decimal, ties to even,
     // "-" for a set sign bit (Python prints -0.0 as "-0.0").  x * 10 is split
     // into its rounded product p and the exact remainder e = fma(x, 10, -p),
