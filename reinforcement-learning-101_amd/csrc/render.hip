@@ -79,6 +79,9 @@ struct Text {
 // straight from the atlas in global memory, a HUD block waited on a chain of
 // dependent loads per pass (strings x pixels x passes).
 constexpr int kRaster = 16384;
+// Rows of a string the raster fill loads at once per column: all that one block's pixels touch when the
+// image is 800 wide (8,192 consecutive pixels: at most 12 rows); narrower images take several rounds.
+constexpr int kBlockRows = 12;
 
 // ---- f-string formatting (Python's int() / str(int) / format(x, '.Nf')) ----
 struct Str {
@@ -358,11 +361,18 @@ __global__ __launch_bounds__(kBlock) void render_kernel(Args p, View<T> v) {
             const Text& t = texts[k2];
             if (t.roff < 0 || t.w == 0) continue;
             const int rows = max(0, min(t.y0 + t.h, row_hi + 1) - t.r0);
-            for (int u = threadIdx.x; u < t.w; u += kBlock) {  // a column per lane, its rows in turn
+            for (int u = threadIdx.x; u < t.w; u += kBlock) {  // a column per lane: its rows loaded together
                 const int i = colchar[k2][u];
                 const int adv = fl.advance[t.glyph[i]];
                 const uint8_t* src = font::kAtlas + fl.offset[t.glyph[i]] + (t.r0 - t.y0) * adv + (u - t.start[i]);
-                for (int r = 0; r < rows; ++r) raster[t.roff + r * t.w + u] = src[r * adv];
+                for (int rb = 0; rb < rows; rb += kBlockRows) {
+                    uint8_t col[kBlockRows];
+#pragma unroll
+                    for (int r = 0; r < kBlockRows; ++r) col[r] = rb + r < rows ? src[(rb + r) * adv] : 0;
+#pragma unroll
+                    for (int r = 0; r < kBlockRows; ++r)
+                        if (rb + r < rows) raster[t.roff + (rb + r) * t.w + u] = col[r];
+                }
             }
         }
         __syncthreads();
