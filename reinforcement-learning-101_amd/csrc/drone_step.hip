@@ -323,11 +323,23 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     const bool oob = (s.x < -c.oob_margin) | (s.x > c.world_width + c.oob_margin) |
                      (s.y < -c.oob_margin) | (s.y > c.world_height + c.oob_margin);
     double term = trig::div_exact(c.shaping_offset - s.dist, c.shaping_scale, k.inv_shaping);
-    term = oob ? c.reward_out_of_bounds : term;
-    term = no_fuel ? c.reward_out_of_fuel : term;
-    term = crash ? c.reward_crash : term;
-    term = landing ? c.reward_landing : term;
     const bool terminal = landing | crash | no_fuel | oob;
+    if constexpr (kRef) {
+        // config.py's terminal rewards are integers: pick one as an int (one
+        // literal per select) and widen it once, instead of selecting doubles
+        // (two literal moves and two selects each): dd_rollout 65,536 x 256
+        // 0.372 -> 0.365 ms, 262,144 x 256 0.952 -> 0.928 ms
+        constexpr DDConfig r = reference_config();
+        static_assert(r.reward_landing == 100.0 && r.reward_crash == -100.0 && r.reward_out_of_fuel == -50.0 &&
+                      r.reward_out_of_bounds == -50.0, "integer terminal rewards");
+        const int32_t ti = landing ? 100 : crash ? -100 : -50;
+        term = terminal ? (double)ti : term;
+    } else {
+        term = oob ? c.reward_out_of_bounds : term;
+        term = no_fuel ? c.reward_out_of_fuel : term;
+        term = crash ? c.reward_crash : term;
+        term = landing ? c.reward_landing : term;
+    }
     s.status |= landing ? (DD_ST_LANDED | DD_ST_DONE) : terminal ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
     const double reward = c.reward_step + term;
     s.total += reward;
