@@ -8,6 +8,7 @@
  *   DroneGame.reset    game_engine.py:59-93    -> dd_reset
  *   DroneGame.get_state game_engine.py:140-177 -> dd_write_obs
  *   DroneGame._get_info game_engine.py:281-298 -> dd_get_info
+ *   DroneGame.render    game_engine.py:300-337 -> dd_render ('rgb_array' frames)
  *   config.py:17-68 module constants           -> DDConfig (dd_config_default)
  *
  * and for the notebooks' side of the loop:
