@@ -24,15 +24,15 @@ def main():
     for frames in (1, 16, 64, 256):
         lanes = torch.arange(0, 4096, 4096 // frames, dtype=torch.int32, device=dev)[:frames]
         out = torch.empty(frames, 600, 800, 3, dtype=torch.uint8, device=dev)
-        for hud in (True, False):
+        for hud, over in ((True, True), (False, True), (False, False)):
             with torch.cuda.stream(stream):
-                env.render(lanes=lanes, out=out, hud=hud, actions=acts)
+                env.render(lanes=lanes, out=out, hud=hud, game_over=over, actions=acts)
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
                 reps = 20
                 with torch.cuda.graph(g, stream=stream):
                     for _ in range(reps):
-                        env.render(lanes=lanes, out=out, hud=hud, actions=acts)
+                        env.render(lanes=lanes, out=out, hud=hud, game_over=over, actions=acts)
                 g.replay()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,7 +42,7 @@ def main():
                 torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / reps
             gbs = frames * 1.44e6 / (us * 1e-6) / 1e9
-            print(json.dumps({"frames": frames, "hud": hud, "us": round(us, 2), "frames_per_s": round(frames / us * 1e6),
+            print(json.dumps({"frames": frames, "hud": hud, "game_over": over, "us": round(us, 2), "frames_per_s": round(frames / us * 1e6),
                               "gbs": round(gbs, 1), "done_lanes": int(env.done[lanes.long()].sum())}), flush=True)
 
 
