@@ -9,8 +9,8 @@ per GPU over its resident shard (state, actions and outputs already in HBM).
 Default workload = BASELINE config 3 per GPU — 262,144 drones, randomised
 spawn, auto-reset, uniform random 3-bit actions, the [N,15] observation
 written every frame — so N=8 is config 4 (2,097,152 drones, weak scaling).
-Steps are replayed from a hipGraph (torch.cuda.CUDAGraph) of ``--graph-steps``
-launches; K steps are timed between barriers + device syncs, the max over
+Steps are replayed from hipGraphs (torch.cuda.CUDAGraph) of min(``--graph-steps``,
+K) launches plus one of the remainder; K steps are timed between barriers + device syncs, the max over
 ranks is reported.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -559,30 +559,40 @@ def main():
         env.step(rows[counter[0] % args.action_rows], write_obs=write_obs)
         counter[0] += 1
 
-    G = args.graph_steps
-    graph = None
+    # Timed launches replay from hipGraphs of G = min(--graph-steps, K) steps
+    # plus one graph of the K % G remainder, so the timed region has the same
+    # shape (graph launches, no per-step host gaps) whatever K is.  (Sizing G
+    # to the warmup too, so the warmup replays the timed graph, was slower at
+    # K = 20, W = 5: four 5-launch replays leave gaps, profiles/r02/k20.)
+    G = min(args.graph_steps, max(args.steps, 1))
+    graphs = {}
+
+    def graph_of(k: int):
+        if k not in graphs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                for i in range(k):
+                    env.step(rows[i % args.action_rows], write_obs=write_obs)
+            graphs[k] = g
+        return graphs[k]
+
     with torch.cuda.stream(stream):
         if G > 0:
             for _ in range(3):  # settle allocations before capture
                 one_step()
             torch.cuda.synchronize(dev)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=stream):
-                for i in range(G):
-                    env.step(rows[i % args.action_rows], write_obs=write_obs)
-            single = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(single, stream=stream):
-                env.step(rows[0], write_obs=write_obs)
+            for k in {G, args.steps % G, args.warmup % G} - {0}:
+                graph_of(k)
 
         def run(k: int):
-            if graph is None:
+            if G <= 0:
                 for _ in range(k):
                     one_step()
                 return
             for _ in range(k // G):
-                graph.replay()
-            for _ in range(k % G):
-                single.replay()
+                graphs[G].replay()
+            if k % G:
+                graphs[k % G].replay()
 
         run(args.warmup)
         torch.cuda.synchronize(dev)

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 4
+#define DD_ABI_VERSION 5
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -190,6 +190,15 @@ typedef struct DDRolloutIO {
     float *obs;           /* float [frames][N][15] (nullable)                   */
     uint64_t action_seed; /* DD_ACT_PHILOX key                                  */
     int64_t action_step;  /* DD_ACT_PHILOX counter of frame 0 (frame k: +k)     */
+    /* Notebook reward mode (as DDStepIO's shaped_*; NULL = engine reward):
+     * reward / done then receive calc_reward (Actor_Critic_PPO.ipynb:164-263)
+     * and the notebook's done with the max_steps timeout (:886-888), and the
+     * [2][N] history is read at launch and written back at its end.          */
+    double *shaped_hist;  /* double [2][N] (nullable)                           */
+    void *engine_reward;  /* shaped mode: the engine's reward [frames][N] (nullable) */
+    uint8_t *engine_done; /* and done; both or neither                          */
+    int32_t max_steps;    /* shaped mode: episode cap, <= 0 = none              */
+    int32_t reserved;
 } DDRolloutIO;
 
 /* Fills *cfg with config.py's values (randomize_platform = 1, others 0). */

@@ -41,7 +41,10 @@ constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
 // (physics.py:16-18).  DD_TRIG_OCML selects the ROCm device library's
 // general-argument sincos instead of trig.h's (timing experiments).
 __device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
-#ifdef DD_TRIG_OCML
+#if defined(DD_EXP_FAKE_TRIG)  // timing-only sensitivity: what the trig costs
+    *s = deg * 1e-3;
+    *c = 1.0 - fabs(*s);
+#elif defined(DD_TRIG_OCML)
     ::sincos(deg * kDeg2Rad, s, c);
 #else
     trig::sincos(deg * kDeg2Rad, s, c);
@@ -168,8 +171,13 @@ struct Lane {
 // of the current state; both the reward and get_state use them.
 __device__ __forceinline__ void measure(Lane& s) {
     const double dx = s.px - s.x, dy = s.py - s.y;
+#ifdef DD_EXP_FAKE_SQRT  // timing-only sensitivity: what the two square roots cost
+    s.speed = (s.vx * s.vx + s.vy * s.vy) * 0.25;
+    s.dist = (dx * dx + dy * dy) * 0.001;
+#else
     s.speed = sqrt(s.vx * s.vx + s.vy * s.vy);
     s.dist = sqrt(dx * dx + dy * dy);
+#endif
 }
 
 // DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
@@ -451,17 +459,82 @@ __device__ __forceinline__ E& at(E* base, uint32_t i) {
     return *reinterpret_cast<E*>(reinterpret_cast<B*>(base) + (uint32_t)(i * (uint32_t)sizeof(E)));
 }
 
+// A wave-uniform pointer the compiler cannot prove uniform (it comes from
+// threadIdx-derived arithmetic, or is hoisted into a VGPR), moved to SGPRs so
+// loads and stores use the SGPR-base + 32-bit lane offset form and its
+// arithmetic stays on the scalar unit.
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* q) {
+    const uint64_t v = reinterpret_cast<uint64_t>(q);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<P*>(((uint64_t)hi << 32) | lo);
+}
+
+// Store cache policies (gfx950): kPlain = write-back into the XCD's L2 (dirty
+// lines leave at the kernel-end release); kNT = non-temporal hint (still
+// write-back); kWT = sc1, write-through (the bytes leave L2 as the wave
+// stores them, nothing is left dirty for the kernel boundary); kWTNT = both.
+enum StorePolicy { kPlain = 0, kWT = 1, kNT = 2, kWTNT = 3 };
+#ifndef DD_ST_STATE
+#define DD_ST_STATE kPlain  // SoA state fields
+#endif
+#ifndef DD_ST_OUT
+#define DD_ST_OUT kNT  // reward / done streams
+#endif
+#ifndef DD_ST_OBS
+#define DD_ST_OBS kNT  // observation rows (16-byte stores)
+#endif
+
+// A buffer resource over [p, p + 2 GiB): raw buffer stores carry any cache
+// policy (aux: bit1 nt, bit4 sc1).  Word 3 is gfx9's 32-bit data format.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int P, typename E>
+__device__ __forceinline__ void store_as(E* base, uint32_t i, E v) {
+    if constexpr (P == kPlain) {
+        at(base, i) = v;
+    } else if constexpr (P == kNT) {
+        __builtin_nontemporal_store(v, &at(base, i));
+    } else if constexpr (P == kWT) {
+        __hip_atomic_store(&at(base, i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        const uint32_t off = i * (uint32_t)sizeof(E);
+        if constexpr (sizeof(E) == 1)
+            __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), rsrc_of(base), off, 0, 18);
+        else if constexpr (sizeof(E) == 4)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rsrc_of(base), off, 0, 18);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsrc_of(base), off, 0, 18);
+    }
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// One 16-byte observation store at float4 index k of a wave-uniform base.
+template <int P>
+__device__ __forceinline__ void store_obs4(f32x4* base, uint32_t k, f32x4 v) {
+    if constexpr (P == kPlain) {
+        at(base, k) = v;
+    } else if constexpr (P == kNT) {
+        __builtin_nontemporal_store(v, &at(base, k));
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base), k * 16u, 0,
+                                               P == kWT ? 16 : 18);
+    }
+}
+
 // Output streams this kernel never re-reads (reward, done) are stored
 // non-temporally, like the obs tile (+2-3 % at 262k and 16M lanes, lab3);
-// DD_PLAIN_OUT_STORES restores plain stores for A/B runs.
+// DD_ST_OUT selects another policy for A/B runs.
 template <typename E>
 __device__ __forceinline__ void put_out(E* base, uint32_t i, E v) {
     asm volatile("" : "+v"(i));  // keep the offset 32-bit and local: SGPR-base store
-#ifdef DD_PLAIN_OUT_STORES
-    at(base, i) = v;
-#else
-    __builtin_nontemporal_store(v, &at(base, i));
-#endif
+    store_as<DD_ST_OUT>(base, i, v);
 }
 
 template <typename T>
@@ -471,10 +544,16 @@ __device__ __forceinline__ void load_dynamics(const Soa<T>& a, uint32_t i, Lane&
     s.px = at(a.px, i); s.py = at(a.py, i);
 }
 
+template <typename E>
+__device__ __forceinline__ void put_state(E* base, uint32_t i, E v) {
+    store_as<DD_ST_STATE>(base, i, v);
+}
+
 template <typename T>
 __device__ __forceinline__ void store_dynamics(const Soa<T>& a, uint32_t i, const Lane& s) {
-    at(a.x, i) = (T)s.x; at(a.y, i) = (T)s.y; at(a.vx, i) = (T)s.vx; at(a.vy, i) = (T)s.vy;
-    at(a.angle, i) = (T)s.angle; at(a.omega, i) = (T)s.omega; at(a.fuel, i) = (T)s.fuel;
+    put_state(a.x, i, (T)s.x); put_state(a.y, i, (T)s.y); put_state(a.vx, i, (T)s.vx);
+    put_state(a.vy, i, (T)s.vy); put_state(a.angle, i, (T)s.angle); put_state(a.omega, i, (T)s.omega);
+    put_state(a.fuel, i, (T)s.fuel);
 }
 
 template <typename T>
@@ -523,8 +602,8 @@ __device__ __forceinline__ void flush_obs_wave(const float* wtile, float* dst, i
     if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
         const int nv = nf >> 2;
         const f32x4* src4 = reinterpret_cast<const f32x4*>(wtile);
-        f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
-        for (int k = lane; k < nv; k += kWave) __builtin_nontemporal_store(src4[k], &dst4[k]);
+        f32x4* dst4 = reinterpret_cast<f32x4*>(uniform_ptr(dst));
+        for (int k = lane; k < nv; k += kWave) store_obs4<DD_ST_OBS>(dst4, (uint32_t)k, src4[k]);
         for (int k = (nv << 2) + lane; k < nf; k += kWave) dst[k] = wtile[k];
     } else {
         for (int k = lane; k < nf; k += kWave) dst[k] = wtile[k];
@@ -668,12 +747,12 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
         uint32_t j = i;
         asm volatile("" : "+v"(j));  // an offset defined in this block: isel folds it into saddr stores
         store_dynamics(a, j, s);
-        at(a.steps, j) = s.steps;
-        at(a.total, j) = (T)s.total;
+        put_state(a.steps, j, s.steps);
+        put_state(a.total, j, (T)s.total);
         const bool moving = !kRef && sw.platform_moving;
-        if (moving || respawned) at(a.px, j) = (T)s.px;
-        if (moving || ended || respawned) at(a.status, j) = (uint8_t)s.status;
-        if (respawned) { at(a.py, j) = (T)s.py; at(a.episode, j) = s.episode; }
+        if (moving || respawned) put_state(a.px, j, (T)s.px);
+        if (moving || ended || respawned) put_state(a.status, j, (uint8_t)s.status);
+        if (respawned) { put_state(a.py, j, (T)s.py); put_state(a.episode, j, s.episode); }
     }
     put_out(static_cast<T*>(p.reward), i, (T)reward);
     put_out(p.done, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
@@ -744,19 +823,13 @@ struct RolloutArgs {
     int32_t n;                // lanes in this chunk
     uint64_t action_seed;
     int64_t action_step;
+    // reward_mode="notebook" (kShaped): reward / done above receive the
+    // notebook's calc_reward and done; the engine's go to these (nullable)
+    double* shaped_hist;      // slot 0 of this chunk; slot 1 at + n_total
+    char* engine_reward;      // frame 0, lane 0 of this chunk (reward_stride apart)
+    uint8_t* engine_done;
+    int32_t max_steps;
 };
-
-// A wave-uniform pointer the compiler cannot prove uniform (it comes from
-// threadIdx-derived arithmetic, or is hoisted into a VGPR), moved to SGPRs so
-// loads and stores use the SGPR-base + 32-bit lane offset form and its
-// arithmetic stays on the scalar unit.
-template <typename P>
-__device__ __forceinline__ P* uniform_ptr(P* q) {
-    const uint64_t v = reinterpret_cast<uint64_t>(q);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return reinterpret_cast<P*>(((uint64_t)hi << 32) | lo);
-}
 
 template <int AFMT>
 __device__ __forceinline__ uint32_t rollout_action(const RolloutArgs& p, int64_t env, int f, uint32_t i) {
@@ -843,8 +916,8 @@ __device__ __forceinline__ void store_held_wave(const HeldObs& h, float* dst, in
     f32x4* dst4 = reinterpret_cast<f32x4*>(uniform_ptr(dst));
     if (nf == kWave * DD_OBS_DIM) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) __builtin_nontemporal_store(h.v[j], &at(dst4, lane + j * kWave));
-        if (lane < kWave * DD_OBS_DIM / 4 - 3 * kWave) __builtin_nontemporal_store(h.v[3], &at(dst4, lane + 3 * kWave));
+        for (int j = 0; j < 3; ++j) store_obs4<DD_ST_OBS>(dst4, lane + j * kWave, h.v[j]);
+        if (lane < kWave * DD_OBS_DIM / 4 - 3 * kWave) store_obs4<DD_ST_OBS>(dst4, lane + 3 * kWave, h.v[3]);
         return;
     }
     const int nv = nf >> 2;
@@ -859,7 +932,7 @@ __device__ __forceinline__ void store_held_wave(const HeldObs& h, float* dst, in
 #ifndef DD_ROLL_MIN_WAVES
 #define DD_ROLL_MIN_WAVES 1  // per SIMD; 4 caps the kernel at 128 VGPRs (A/B: DESIGN.md section 4)
 #endif
-template <typename T, int AFMT, bool kRef, bool kHeld>
+template <typename T, int AFMT, bool kRef, bool kHeld, bool kShaped>
 __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(RolloutArgs p, Soa<T> a) {
     __shared__ __attribute__((aligned(16))) float tile[kHeld ? 2 : 1][kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0)];
     const DDConfig& sw = p.k.c;
@@ -878,8 +951,12 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     const int woff = (int)__builtin_amdgcn_readfirstlane((threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM);
     const int roff = threadIdx.x * DD_OBS_DIM;                   // the lane's row in a tile
     const int64_t env = a.env_id_base + i;
+    constexpr bool kGuard = !kRef && std::is_same<T, double>::value;
     HeldObs held;
     Lane s;
+    // kShaped: the notebook reward's two-frame distance history, in registers
+    double h0 = 0.0, h1 = 0.0;
+    if constexpr (kShaped) { h0 = at(p.shaped_hist, i); h1 = at(p.shaped_hist + p.n_total, i); }
     load_dynamics(a, i, s);
     s.total = at(a.total, i);
     s.status = at(a.status, i);
@@ -910,11 +987,11 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
         const uint32_t act = slot;
         slot = rollout_action<AFMT>(p, env, min(f + 2, p.frames - 1), i);
         double reward;
+        const bool was_done = (s.status & DD_ST_DONE) != 0;
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
             // frame (a done lane's result is discarded), and a wave with a lane
             // to re-spawn takes the one branch
-            const bool was_done = (s.status & DD_ST_DONE) != 0;
             reward = frame<kRef, true>(k, sw, act, s);
             if (__ballot(was_done)) {
                 if (was_done) {
@@ -922,15 +999,49 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
                     reward = 0.0;
                 }
             }
-        } else if (s.status & DD_ST_DONE) {  // sticky done (game_engine.py:107-111)
+        } else if (was_done) {  // sticky done (game_engine.py:107-111)
             measure(s);
             reward = 0.0;
         } else {
             reward = frame<kRef, true>(k, sw, act, s);
         }
-        put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
-        put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-        if constexpr (kObs) observe<!kRef && std::is_same<T, double>::value>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+        if constexpr (kShaped) {
+            // dd_step's notebook path (finish_lane) with the history in h0 / h1:
+            // slot steps & 1 holds the distance two frames back
+            double v[13];
+            observe_values<kGuard>(k, s, v);
+            double shaped = 0.0;
+            bool shaped_done;
+            if (kAuto && was_done) {  // re-spawned: the history restarts (prev_state None)
+                h0 = v[9];
+                h1 = __builtin_nan("");
+                shaped_done = false;
+            } else if (was_done) {  // sticky done
+                shaped_done = true;
+            } else {
+                const bool odd = (s.steps & 1) != 0;
+                shaped = notebook_reward(v, s.status, odd ? h1 : h0);
+                h1 = odd ? v[9] : h1;
+                h0 = odd ? h0 : v[9];
+                shaped_done = (s.status & DD_ST_DONE) != 0;
+                if (p.max_steps > 0 && s.steps >= p.max_steps) {  // collect_episodes_ppo timeout
+                    shaped = (s.status & DD_ST_LANDED) ? shaped : shaped - 500;
+                    shaped_done = true;
+                    s.status |= DD_ST_DONE;
+                }
+            }
+            put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)shaped);
+            put_out(p.done + f * p.n_total, i, (uint8_t)(shaped_done ? 1 : 0));
+            if (p.engine_reward) {
+                put_out(reinterpret_cast<T*>(p.engine_reward + f * p.reward_stride), i, (T)reward);
+                put_out(p.engine_done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+            }
+            if constexpr (kObs) write_obs_row(v, s.status, tile[kHeld ? (f & 1) : 0] + roff);
+        } else {
+            put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
+            put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+            if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+        }
         quantize<T, kRef>(s);  // the obs above sees the unrounded frame, like dd_step's
         if constexpr (kObs) {
             if constexpr (kHeld) {
@@ -961,7 +1072,10 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
         hold_obs_wave(tile[f & 1] + woff, wfloats, held);
         store_held_wave(held, p.obs + ((size_t)f * p.n_total + wrow0) * DD_OBS_DIM, wfloats);
     }
-    if (live) store_spawn(reload_soa<RolloutArgs, T>(), i, s);  // every field: lanes may have re-spawned
+    if (live) {
+        store_spawn(reload_soa<RolloutArgs, T>(), i, s);  // every field: lanes may have re-spawned
+        if constexpr (kShaped) { at(p.shaped_hist, i) = h0; at(p.shaped_hist + p.n_total, i) = h1; }
+    }
 }
 
 // dd_shaped_reset kernel: the notebook reward's history restarts from the
@@ -1198,22 +1312,24 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
     }
 }
 
-template <typename T, int AFMT, bool kRef>
+template <typename T, int AFMT, bool kRef, bool kShaped>
 void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
     // the held obs path needs every frame row start 16-byte aligned
     const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0;
     const unsigned blocks = (unsigned)tiles_of(p.n);
-    if (held) hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true>), dim3(blocks), dim3(kBlock), 0, s, p, a);
-    else hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false>), dim3(blocks), dim3(kBlock), 0, s, p, a);
+    if (held)
+        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true, kShaped>), dim3(blocks), dim3(kBlock), 0, s, p, a);
+    else
+        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false, kShaped>), dim3(blocks), dim3(kBlock), 0, s, p, a);
 }
 
-template <typename T, bool kRef>
+template <typename T, bool kRef, bool kShaped>
 void launch_rollout_fmt(const RolloutArgs& p, int afmt, const Soa<T>& a, hipStream_t s) {
     switch (afmt) {
-        case DD_ACT_BITMASK: launch_rollout<T, DD_ACT_BITMASK, kRef>(p, a, s); break;
-        case DD_ACT_F32X3: launch_rollout<T, DD_ACT_F32X3, kRef>(p, a, s); break;
-        case DD_ACT_U8X3: launch_rollout<T, DD_ACT_U8X3, kRef>(p, a, s); break;
-        default: launch_rollout<T, DD_ACT_PHILOX, kRef>(p, a, s); break;
+        case DD_ACT_BITMASK: launch_rollout<T, DD_ACT_BITMASK, kRef, kShaped>(p, a, s); break;
+        case DD_ACT_F32X3: launch_rollout<T, DD_ACT_F32X3, kRef, kShaped>(p, a, s); break;
+        case DD_ACT_U8X3: launch_rollout<T, DD_ACT_U8X3, kRef, kShaped>(p, a, s); break;
+        default: launch_rollout<T, DD_ACT_PHILOX, kRef, kShaped>(p, a, s); break;
     }
 }
 
@@ -1232,9 +1348,20 @@ void rollout_chunks(RolloutArgs p, const DDState& st, const DDRolloutIO& io, int
         p.done = io.done + first;
         p.obs = io.obs ? io.obs + first * DD_OBS_DIM : nullptr;
         p.n = (int32_t)len;
+        const bool shaped = io.shaped_hist != nullptr;
+        p.shaped_hist = shaped ? io.shaped_hist + first : nullptr;
+        p.engine_reward = shaped && io.engine_reward
+                              ? reinterpret_cast<char*>(static_cast<T*>(io.engine_reward) + first) : nullptr;
+        p.engine_done = shaped && io.engine_reward ? io.engine_done + first : nullptr;
+        p.max_steps = io.max_steps;
         const Soa<T> a = soa_of<T>(st, first);
-        if (ref) launch_rollout_fmt<T, true>(p, io.action_format, a, s);
-        else launch_rollout_fmt<T, false>(p, io.action_format, a, s);
+        if (ref) {
+            if (shaped) launch_rollout_fmt<T, true, true>(p, io.action_format, a, s);
+            else launch_rollout_fmt<T, true, false>(p, io.action_format, a, s);
+        } else {
+            if (shaped) launch_rollout_fmt<T, false, true>(p, io.action_format, a, s);
+            else launch_rollout_fmt<T, false, false>(p, io.action_format, a, s);
+        }
     }
 }
 
@@ -1278,6 +1405,8 @@ int dd_rollout(const DDConfig* cfg, const DDState* st, const DDRolloutIO* io, in
     if (n == 0 || io->frames == 0) return 0;
     if (!dd::state_ok(st) || !io->reward || !io->done) return hipErrorInvalidValue;
     if (io->action_format != DD_ACT_PHILOX && !io->actions) return hipErrorInvalidValue;
+    if ((io->engine_reward != nullptr) != (io->engine_done != nullptr)) return hipErrorInvalidValue;
+    if (io->engine_reward && !io->shaped_hist) return hipErrorInvalidValue;
     hipStream_t s = static_cast<hipStream_t>(stream);
     dd::RolloutArgs p{};
     p.k = dd::make_consts(*cfg);

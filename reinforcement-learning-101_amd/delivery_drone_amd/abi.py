@@ -20,7 +20,7 @@ __all__ = [
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 4
+DD_ABI_VERSION = 5
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
@@ -87,6 +87,8 @@ class DDRolloutIO(ctypes.Structure):
         ("actions", ctypes.c_void_p), ("action_format", _I), ("frames", _I),
         ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("obs", ctypes.c_void_p),
         ("action_seed", ctypes.c_uint64), ("action_step", ctypes.c_int64),
+        ("shaped_hist", ctypes.c_void_p), ("engine_reward", ctypes.c_void_p), ("engine_done", ctypes.c_void_p),
+        ("max_steps", _I), ("reserved", _I),
     ]
 
 

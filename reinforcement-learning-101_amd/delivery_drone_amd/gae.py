@@ -47,6 +47,19 @@ def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, gamma:
         raise ValueError(f"dones must be [T, N], got {tuple(dones.shape)}")
     if out is not None:
         adv, ret = out
+
+        def _check(t, what):
+            if (not isinstance(t, torch.Tensor) or t.dtype != torch.float32 or tuple(t.shape) != (T, n)
+                    or not t.is_contiguous() or t.device != dev):
+                raise ValueError(f"out {what} must be a contiguous float32 tensor of shape {(T, n)} on {dev}")
+
+        _check(adv, "advantages")
+        if returns:
+            if ret is None:
+                raise ValueError("out=(adv, None) with returns=True: pass a returns buffer")
+            _check(ret, "returns")
+        else:
+            ret = None
     else:
         adv = torch.empty(T, n, dtype=torch.float32, device=dev)
         ret = torch.empty_like(adv) if returns else None

@@ -109,6 +109,12 @@ def test_argument_errors_return_invalid_value_without_gpu():
     assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
     rio.action_format, rio.frames = 3, -1
     assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.frames = 4
+    rio.engine_reward = 8  # engine outputs: both or neither, and only in notebook (shaped) mode
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.engine_done = 8
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.engine_reward = rio.engine_done = None
     rio.frames = 0  # nothing to do
     assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == 0
     io.done_idx = None

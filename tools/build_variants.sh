@@ -23,9 +23,9 @@ for v in ${VARIANTS:-base}; do
   case $v in
     base) build base ;;
     ocml) build ocml -DDD_TRIG_OCML ;;
-    plainobs) build plainobs -DDD_PLAIN_OBS_STORES ;;
+    plainobs) build plainobs -DDD_ST_OBS=0 ;;
     nofma) build nofma -DDD_TRIG_NO_FMA ;;
-    plainout) build plainout -DDD_PLAIN_OUT_STORES ;;
+    plainout) build plainout -DDD_ST_OUT=0 ;;
     nomath) build nomath -DDD_EXP_NOMATH ;;
     obsmul) build obsmul -DDD_OBS_MUL ;;
     mlpw4) build mlpw4 -DDD_MLP_WAVES=4 ;;
@@ -40,6 +40,15 @@ for v in ${VARIANTS:-base}; do
     rw4) build rw4 -DDD_ROLL_MIN_WAVES=4 ;;
     lateact) build lateact -DDD_EXP_LATE_ACT ;;
     wrapsel) build wrapsel -DDD_EXP_STEP_WRAP_SELECT ;;
+    wts) build wts -DDD_ST_STATE=1 ;;
+    wto) build wto -DDD_ST_OUT=1 -DDD_ST_OBS=1 ;;
+    wtall) build wtall -DDD_ST_STATE=1 -DDD_ST_OUT=1 -DDD_ST_OBS=1 ;;
+    wtntall) build wtntall -DDD_ST_STATE=3 -DDD_ST_OUT=3 -DDD_ST_OBS=3 ;;
+    wtsnto) build wtsnto -DDD_ST_STATE=1 -DDD_ST_OUT=3 -DDD_ST_OBS=3 ;;
+    plainall) build plainall -DDD_ST_OUT=0 -DDD_ST_OBS=0 ;;
+    faketrig) build faketrig -DDD_EXP_FAKE_TRIG ;;
+    fakesqrt) build fakesqrt -DDD_EXP_FAKE_SQRT ;;
+    emptyb1024) build emptyb1024 -DDD_EXP_EMPTY -DDD_STEP_BLOCK=1024 ;;
     *) echo "unknown variant $v" >&2; exit 1 ;;
   esac
 done
