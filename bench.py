@@ -350,9 +350,10 @@ def notebook_point(n, precision, seed, dev):
 
 MLP_FLOPS_PER_ROW = 2 * (15 * 128 + 128 * 128 + 128 * 64 + 64 * 3)  # the notebooks' actor, algorithmic
 F32_MFMA_PEAK_TFS = 157.3  # MI355X dense f32 MFMA (MI355X_MICROARCH.md, Matrix cores)
+F16_MFMA_PEAK_TFS = 2516.6  # dense f16 MFMA, ~2.5 PF (MI355X_MICROARCH.md: 32x32x16 at 32 cycles/SIMD, 2.4 GHz)
 
 
-def _random_actor(dev, seed):
+def _random_actor(dev, seed, compute="f32"):
     """The notebooks' DroneGamerBoi body with torch's default init (random
     weights of that architecture; no checkpoint travels to the box)."""
     import torch
@@ -361,14 +362,16 @@ def _random_actor(dev, seed):
     torch.manual_seed(seed)
     net = nn.Sequential(nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128), nn.LayerNorm(128),
                         nn.ReLU(), nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(), nn.Linear(64, 3))
-    return MlpNet(net.state_dict(), device=dev)
+    return MlpNet(net.state_dict(), device=dev, compute=compute)
 
 
-def policy_point(n, seed, dev):
+def policy_point(n, seed, dev, compute="f32"):
     """the actor forward + Bernoulli sample + log-prob
-    (dd_mlp_forward) over n observation rows; bound = f32 MFMA."""
+    (dd_mlp_forward) over n observation rows; bound = the MFMA of `compute`
+    (f32: 157.3 TF dense; f16x3: three f16 MFMAs per product, priced against
+    the f16 MFMA's 2.5 PF at 3x the algorithmic flops)."""
     import torch
-    actor = _random_actor(dev, seed)
+    actor = _random_actor(dev, seed, compute)
     obs = torch.randn(n, 15, device=dev)
     acts = torch.empty(n, dtype=torch.uint8, device=dev)
     lp = torch.empty(n, device=dev)
@@ -393,19 +396,26 @@ def policy_point(n, seed, dev):
     tfs = n * MLP_FLOPS_PER_ROW / (us * 1e-6) / 1e12
     del actor, obs, acts, lp, g
     torch.cuda.empty_cache()
-    return {"rows": n, "us": round(us, 2), "launch": "hipGraph of 50 dd_mlp_forward", "rows_per_s": round(n / (us * 1e-6), 1),
-            "roofline": {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_row": MLP_FLOPS_PER_ROW},
-            "kernel": "dd::mlp::mlp_kernel<3> (dd_mlp_forward: actor + Bernoulli sample + log-prob, f32 MFMA)"}
+    if compute == "f32":
+        roof = {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_row": MLP_FLOPS_PER_ROW}
+        kernel = "dd::mlp::mlp_kernel<3, false> (dd_mlp_forward: actor + Bernoulli sample + log-prob, f32 MFMA)"
+    else:  # the MFMA pipe runs 3x the algorithmic flops (hi.hi, hi.lo, lo.hi)
+        roof = {"bound": "mfma", "achieved": round(3 * tfs, 2), "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(3 * tfs / F16_MFMA_PEAK_TFS, 4), "flops_per_row": 3 * MLP_FLOPS_PER_ROW,
+                "algorithmic_tflops": round(tfs, 2)}
+        kernel = "dd::mlp::mlp_kernel<3, true> (dd_mlp_forward, DD_MLP_F16X3: split f16 operands on the f16 MFMA)"
+    return {"rows": n, "compute": compute, "us": round(us, 2), "launch": "hipGraph of 50 dd_mlp_forward",
+            "rows_per_s": round(n / (us * 1e-6), 1), "roofline": roof, "kernel": kernel}
 
 
-def policy_rollout_point(n, frames, seed, dev):
+def policy_rollout_point(n, frames, seed, dev, compute="f32"):
     """Policy in the loop, nothing on the host: per frame dd_mlp_forward
     (sample from the current obs) then dd_step, `frames` frames captured in
     one hipGraph.  env-steps/s with the actor's inference included."""
     import torch
     from delivery_drone_amd import EnvConfig, VecDroneEnv
-    actor = _random_actor(dev, seed)
+    actor = _random_actor(dev, seed, compute)
     cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
     env = VecDroneEnv(n, device=dev, config=cfg)
     obs = env.reset()
@@ -434,8 +444,8 @@ def policy_rollout_point(n, frames, seed, dev):
     ms = e0.elapsed_time(e1) / reps
     del actor, env, acts, lp, g
     torch.cuda.empty_cache()
-    return {"envs": n, "frames": frames, "ms": round(ms, 3), "steps_per_s": round(n * frames / (ms * 1e-3), 1),
-            "us_per_frame": round(ms * 1e3 / frames, 2),
+    return {"envs": n, "frames": frames, "compute": compute, "ms": round(ms, 3),
+            "steps_per_s": round(n * frames / (ms * 1e-3), 1), "us_per_frame": round(ms * 1e3 / frames, 2),
             "launch": f"hipGraph of {frames} x (dd_mlp_forward + dd_step)"}
 
 
@@ -629,7 +639,7 @@ def main():
             gp = gather_point(env, n, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
             gp = {"error": f"{type(e).__name__}: {e}"[:300]}
-    c5 = c5a = g5 = c2 = nb = pp = pr = sp = rp = None
+    c5 = c5a = g5 = c2 = nb = pp = pr = pp16 = pr16 = sp = rp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         c5a = step_loop_point(args.rollout_point, 256, args.precision, args.seed, dev)
@@ -639,6 +649,8 @@ def main():
         nb = notebook_point(n, args.precision, args.seed, dev)
         pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
         pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
+        pp16 = policy_point(args.rollout_point or 65_536, args.seed, dev, "f16x3")
+        pr16 = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev, "f16x3")
         sp = socket_point(args.seed, dev)
         rp = render_point(args.seed, dev)
 
@@ -696,6 +708,8 @@ def main():
             "notebook_reward_point": nb,
             "policy_point": pp,
             "policy_rollout_point": pr,
+            "policy_point_f16x3": pp16,
+            "policy_rollout_point_f16x3": pr16,
             "socket_point": sp,
             "render_point": rp,
             "gpu_ms_per_step": round(step_ms, 6),

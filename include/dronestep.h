@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 5
+#define DD_ABI_VERSION 6
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -289,13 +289,22 @@ typedef struct DDMlpIO {
     int64_t env_id_base;
 } DDMlpIO;
 
-/* Floats of a packed parameter buffer (same for K = 1 and 3). */
+/* Arithmetic of the three hidden GEMMs.  DD_MLP_F32: the f32 MFMA, the
+ * notebook's float32 model as is.  DD_MLP_F16X3 (opt-in, ~4x faster): each
+ * operand split into two f16 halves, a = hi + lo * 2^-11, three f16 MFMAs
+ * per product with f32 accumulation (~22 bits per product, about the f32
+ * path's end-to-end error); |weights|, |obs| and activations < 65504.
+ * LayerNorm, the last layer and sampling are f32 either way. */
+enum { DD_MLP_F32 = 0, DD_MLP_F16X3 = 1 };
+
+/* Floats of a packed parameter buffer (same for K = 1 and 3, either compute). */
 int64_t dd_mlp_packed_floats(void);
-/* Repack state_dict tensors into `packed` (device, dd_mlp_packed_floats()). */
-int dd_mlp_pack(const DDMlpParams *params, float *packed, void *stream);
-/* Forward pass; out_dim must match the packed parameters. */
-int dd_mlp_forward(const float *packed, int32_t out_dim, const DDMlpIO *io,
-                   int64_t n, void *stream);
+/* Repack state_dict tensors into `packed` (device, dd_mlp_packed_floats())
+ * for `compute` (DD_MLP_*). */
+int dd_mlp_pack(const DDMlpParams *params, int32_t compute, float *packed, void *stream);
+/* Forward pass; out_dim and compute must match the packed parameters. */
+int dd_mlp_forward(const float *packed, int32_t compute, int32_t out_dim,
+                   const DDMlpIO *io, int64_t n, void *stream);
 
 /* ---- Rendering -------------------------------------
  * DroneGame.render() in 'rgb_array' mode (game_engine.py:300-337): the scene

@@ -25,6 +25,15 @@
 //     4 k-steps so one ds_read_b128 feeds four MFMAs) live in LDS, loaded
 //     once per block of 8 waves (2 per SIMD, 1 block per CU).
 //   * The last layer (64 -> K <= 3) and the sampling run on the VALU.
+//
+// DD_MLP_F16X3 (opt-in) runs the three hidden GEMMs on the f16 MFMA
+// (v_mfma_f32_32x32x16_f16, 16x the f32 MFMA's rate) with every operand
+// split in two halves, a = hi + lo' * 2^-11 (hi = f16(a), lo' = f16((a - hi)
+// * 2^11), both nearest-even): a . b = hi.hi + 2^-11 (hi.lo' + lo'.hi) + O(2^-22),
+// three f16 MFMAs per k-step of 16, products exact and summed in f32, so a
+// dot product carries about the f32 path's error (the notebook's actor
+// probabilities within 5e-7 of float64 either way, tools/mlp_split_sim.py).
+// Operands must stay below 65504 in magnitude (f16 range).
 
 #include <hip/hip_runtime.h>
 #include <float.h>
@@ -51,7 +60,9 @@ constexpr int kCols = 32;  // drones per wave tile
 
 // k-steps of 2 per layer (K = 16 for the 15 inputs + one zero column).
 constexpr int kSteps1 = 8, kSteps2 = 64, kSteps3 = 64;
-// Packed buffer (floats).  A sections are [out tile][k-step group of 4][lane][4].
+// Packed buffer (floats).  A sections are [out tile][k-step group of 4][lane][4]
+// (DD_MLP_F32) or, in the same space, [out tile][k-step of 16][hi | lo'][lane][8
+// halves] (DD_MLP_F16X3, pack_a16); the vector sections are shared.
 constexpr int kA1 = 0;
 constexpr int kA2 = kA1 + 4 * kSteps1 * 64;
 constexpr int kA3 = kA2 + 4 * kSteps2 * 64;
@@ -68,12 +79,81 @@ static_assert(kPacked % 4 == 0, "packed buffer is read as float4");
 // (C/D map of the 32x32 MFMAs on gfx950: row = (r&3) + 8(r>>2) + 4h).
 __host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// ---- DD_MLP_F16X3: split operands on the f16 MFMA --------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr float kLoScale = 2048.0f;  // 2^11: lo' lives at hi's magnitude (no f16 subnormals)
+constexpr float kLoUnscale = 1.0f / 2048.0f;
+
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// Two floats -> packed f16 hi and lo' halves, each rounded to nearest-even
+// (v_cvt_pk_f16_f32).  a - hi is exact in f32 (hi is a to 11 bits), the
+// scaling by 2^11 too.  (Truncating instead, v_cvt_pkrtz, biases lo' and
+// quadruples the end-to-end error: tools/mlp_split_sim.py --truncate.)
+// Written on float pairs so it lowers to v_cvt_pk_f16_f32, two
+// v_cvt_f32_f16, v_pk_add_f32, v_pk_mul_f32, v_cvt_pk_f16_f32 (6 VALU per
+// pair; scalar code had the compiler convert each half twice: 10).
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
+    uint32_t hp = __builtin_bit_cast(uint32_t, f16x2{(_Float16)a, (_Float16)b});
+    asm("" : "+v"(hp));  // widen hi from the packed register (else each half is converted twice)
+    const f16x2 h = __builtin_bit_cast(f16x2, hp);
+    const f32x2 r = (f32x2{a, b} - f32x2{(float)h.x, (float)h.y}) * f32x2{kLoScale, kLoScale};
+    const f16x2 l = {(_Float16)r.x, (_Float16)r.y};
+    hi = hp;
+    lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// Eight consecutive activations (one B fragment of a k-step) -> hi, lo'.
+__device__ __forceinline__ void split8(const float* v, f16x8& hi, f16x8& lo) {
+    u32x4 h, l;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        uint32_t a, b;
+        split_pair(v[2 * m], v[2 * m + 1], a, b);
+        h[m] = a;
+        l[m] = b;
+    }
+    hi = __builtin_bit_cast(f16x8, h);
+    lo = __builtin_bit_cast(f16x8, l);
+}
+
+// W[row][col] of layer 1 (cols >= 15 are the zero padding) or layers 2, 3.
+__device__ __forceinline__ float weight_at(const DDMlpParams& p, int base, int row, int col) {
+    if (base == kA1) return col < kIn ? p.w0[row * kIn + col] : 0.0f;
+    return (base == kA2 ? p.w3 : p.w6)[row * 128 + col];
+}
+
+// DD_MLP_F16X3 A fragments, one packed float = two halves: section
+// [tile][k-step][hi | lo'][lane][8 halves]; lane l of k-step s of out tile t
+// holds W[32t + (l&31)][k] for its elements j, k = 8h + j (layer 1) or hidden
+// row hid(s>>1, 8(s&1) + j, h) (layers 2, 3: the B fragments split_acts makes).
+__device__ __forceinline__ float pack_a16(const DDMlpParams& p, int i) {
+    const int base = i < kA2 ? kA1 : i < kA3 ? kA2 : kA3;
+    const int ks = base == kA1 ? 1 : 8;
+    const int o = i - base;
+    const int blk = o / 512, w = o % 512;
+    const int t = blk / ks, s = blk % ks, part = w / 256, l = (w % 256) / 4, m = w % 4;
+    const int row = 32 * t + (l & 31), h = l >> 5;
+    float v[2];
+    for (int e = 0; e < 2; ++e) {
+        const int j = 2 * m + e;
+        const int col = base == kA1 ? 8 * h + j : hid(s >> 1, 8 * (s & 1) + j, h);
+        v[e] = weight_at(p, base, row, col);
+    }
+    uint32_t hi, lo;
+    split_pair(v[0], v[1], hi, lo);
+    return __uint_as_float(part == 0 ? hi : lo);
+}
+
 // One packed float: which state_dict element (or zero) goes at index i.
-__global__ void pack_kernel(DDMlpParams p, float* out) {
+__global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= kPacked) return;
     float v = 0.0f;
-    if (i < kV1) {  // A operands: lane l of k-step q of out tile t holds W[32t + (l&31)][k(q, l>>5)]
+    if (i < kV1 && compute == DD_MLP_F16X3) {
+        v = pack_a16(p, i);
+    } else if (i < kV1) {  // A operands: lane l of k-step q of out tile t holds W[32t + (l&31)][k(q, l>>5)]
         const int base = i < kA2 ? kA1 : i < kA3 ? kA2 : kA3;
         const int steps = i < kA2 ? kSteps1 : i < kA3 ? kSteps2 : kSteps3;
         const int o = i - base;
@@ -134,6 +214,45 @@ __device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lan
     }
 }
 
+// out^T tiles (NT of 32 rows) = bias + W . in^T over KS k-steps of 16.  The
+// packed A fragments are [tile][k-step][hi | lo'][lane] x 16 B; bh / bl are
+// the lane's B fragments.  The cross terms go first into the zeroed
+// accumulator, which is then scaled by 2^-11 and given the bias, and the
+// hi.hi products accumulate on top: one accumulator per tile.
+template <int NT, int KS>
+__device__ __forceinline__ void layer16(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
+                                        const f16x8 (&bl)[KS], f32x16 (&acc)[NT], const float* bias_h) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const u32x4* blk = a16 + (t * KS + s) * 128;
+            const f16x8 ah = __builtin_bit_cast(f16x8, blk[lane]);
+            const f16x8 al = __builtin_bit_cast(f16x8, blk[64 + lane]);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep each k-step's LDS reads next to its MFMAs
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const f16x8 ah = __builtin_bit_cast(f16x8, a16[(t * KS + s) * 128 + lane]);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // x + (the same register of the other lane half), i.e. x + __shfl_xor(x, 32),
 // as one v_permlane32_swap (gfx950) instead of an LDS permute.  Lanes < 32
 // get x_l + x_{l+32}, lanes >= 32 x_{l-32} + x_l: the same sum (IEEE
@@ -148,9 +267,9 @@ __device__ __forceinline__ float add_other_half(float x) {
 // of registers hold adjacent rows, so the arithmetic runs as packed f32
 // (v_pk_add / v_pk_fma), in torch's form y = (x * rstd - rstd * mean) *
 // weight + bias.
-template <int NT>
-__device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
-                                          float (&y)[NT][16]) {
+template <int NT, typename Emit>
+__device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
+                                               Emit emit) {
     constexpr int kRows = 32 * NT;
     const float* gamma = vec + kRows + 4 * h;
     const float* beta = vec + 2 * kRows + 4 * h;
@@ -175,6 +294,7 @@ __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* 
     const f32x2 rs2 = {rstd, rstd}, nb2 = {-rstd * mean, -rstd * mean};
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+        float y[16];
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
             const int row = hid(t, r, 0);  // rows row, row + 1 (r even)
@@ -182,11 +302,33 @@ __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* 
             const f32x2 b = *reinterpret_cast<const f32x2*>(beta + row);
             const f32x2 xn = __builtin_elementwise_fma(f32x2{acc[t][r], acc[t][r + 1]}, rs2, nb2);
             const f32x2 v = __builtin_elementwise_fma(xn, g, b);
-            y[t][r] = fmaxf(v.x, 0.0f);  // ReLU
-            y[t][r + 1] = fmaxf(v.y, 0.0f);
+            y[r] = fmaxf(v.x, 0.0f);  // ReLU
+            y[r + 1] = fmaxf(v.y, 0.0f);
         }
+        emit(t, y);
         __builtin_amdgcn_sched_barrier(0);  // one tile's parameters in registers at a time
     }
+}
+
+template <int NT>
+__device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
+                                          float (&y)[NT][16]) {
+    norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[t][r] = v[r];
+    });
+}
+
+// norm_relu straight into the next layer's split B fragments: k-step s takes
+// registers 8(s&1)..+7 of tile s>>1 (hidden rows hid(s>>1, 8(s&1)+j, h)),
+// the k order pack_a16 assumes.  No f32 copy of the activations stays live.
+template <int NT>
+__device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
+                                                f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
+    norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
+        split8(&v[0], bh[2 * t], bl[2 * t]);
+        split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
+    });
 }
 
 struct FwdArgs {
@@ -209,7 +351,7 @@ __device__ __forceinline__ float bernoulli_logp(float p, bool on) {
     return on ? logf(pc) : log1pf(-pc);
 }
 
-template <int K>
+template <int K, bool kSplit>
 __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__ packed, FwdArgs p) {
     extern __shared__ f32x4 lds4[];
     const float* lds = reinterpret_cast<const float*>(lds4);
@@ -223,23 +365,42 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
          tile += (int64_t)gridDim.x * kWaves) {
         const int64_t d = tile * kCols + c;  // this lane's drone (column)
         const bool live = d < p.n;
-        float x[kSteps1];  // B operands of layer 1: obs[d][2q + h]
-#pragma unroll
-        for (int q = 0; q < kSteps1; ++q) {
-            const int k = 2 * q + h;
-            x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
-        }
-
         f32x16 acc4[4];
-        float y1[4][16], y2[4][16];
-        layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
-        norm_relu<4>(acc4, lds + kV1, eps, h, y1);
-        layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4, lds + kV2 + 4 * h);
-        norm_relu<4>(acc4, lds + kV2, eps, h, y2);
         f32x16 acc2[2];
         float y3[2][16];
-        layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2, lds + kV3 + 4 * h);
-        norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        if constexpr (kSplit) {
+            float x[8];  // the one k-step of layer 1: obs[d][8h + j]
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 8 * h + j;
+                x[j] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
+            }
+            const u32x4* a16 = reinterpret_cast<const u32x4*>(lds);
+            f16x8 b1h[1], b1l[1], bh[8], bl[8];
+            split8(x, b1h[0], b1l[0]);
+            layer16<4, 1>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
+            norm_relu_split<4>(acc4, lds + kV1, eps, h, bh, bl);
+            layer16<4, 8>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
+            norm_relu_split<4>(acc4, lds + kV2, eps, h, bh, bl);
+            layer16<2, 8>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+            norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        } else {
+            float y1[4][16], y2[4][16];
+            float x[kSteps1];  // B operands of layer 1: obs[d][2q + h]
+#pragma unroll
+            for (int q = 0; q < kSteps1; ++q) {
+                const int k = 2 * q + h;
+                x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
+            }
+            layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
+            norm_relu<4>(acc4, lds + kV1, eps, h, y1);
+            layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4,
+                                   lds + kV2 + 4 * h);
+            norm_relu<4>(acc4, lds + kV2, eps, h, y2);
+            layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2,
+                                   lds + kV3 + 4 * h);
+            norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        }
         __builtin_amdgcn_sched_barrier(0);
 
         float z[K];  // Linear(64, K): 32 rows per lane half, then the other half's
@@ -287,11 +448,11 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
     }
 }
 
-template <int K>
+template <int K, bool kSplit>
 hipError_t launch(const float* packed, const FwdArgs& a, hipStream_t s) {
     static bool configured = false;  // the LDS image exceeds the 64 KB default
     if (!configured) {
-        const hipError_t e = hipFuncSetAttribute((const void*)mlp_kernel<K>,
+        const hipError_t e = hipFuncSetAttribute((const void*)mlp_kernel<K, kSplit>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
         if (e != hipSuccess) return e;
         configured = true;
@@ -302,7 +463,7 @@ hipError_t launch(const float* packed, const FwdArgs& a, hipStream_t s) {
     const int64_t tiles = (a.n + kCols - 1) / kCols;
     const int64_t want = (tiles + kWaves - 1) / kWaves;
     const unsigned blocks = (unsigned)(want < cus ? want : cus);  // one block per CU, waves loop over tiles
-    hipLaunchKernelGGL(mlp_kernel<K>, dim3(blocks), dim3(kThreads), kLdsBytes, s, packed, a);
+    hipLaunchKernelGGL((mlp_kernel<K, kSplit>), dim3(blocks), dim3(kThreads), kLdsBytes, s, packed, a);
     return hipGetLastError();
 }
 
@@ -313,25 +474,30 @@ extern "C" {
 
 int64_t dd_mlp_packed_floats(void) { return dd::mlp::kPacked; }
 
-int dd_mlp_pack(const DDMlpParams* p, float* packed, void* stream) {
+int dd_mlp_pack(const DDMlpParams* p, int32_t compute, float* packed, void* stream) {
     if (!p || !packed || !(p->out_dim == 1 || p->out_dim == 3) || !(p->ln_eps > 0.0f)) return hipErrorInvalidValue;
+    if (compute != DD_MLP_F32 && compute != DD_MLP_F16X3) return hipErrorInvalidValue;
     const float* req[] = {p->w0, p->b0, p->ln1_w, p->ln1_b, p->w3, p->b3, p->ln4_w,
                           p->ln4_b, p->w6, p->b6, p->ln7_w, p->ln7_b, p->w9, p->b9};
     for (const float* q : req)
         if (!q) return hipErrorInvalidValue;
     const int threads = 256, blocks = (dd::mlp::kPacked + threads - 1) / threads;
-    hipLaunchKernelGGL(dd::mlp::pack_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, *p, packed);
+    hipLaunchKernelGGL(dd::mlp::pack_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, *p, compute, packed);
     return hipGetLastError();
 }
 
-int dd_mlp_forward(const float* packed, int32_t out_dim, const DDMlpIO* io, int64_t n, void* stream) {
+int dd_mlp_forward(const float* packed, int32_t compute, int32_t out_dim, const DDMlpIO* io, int64_t n,
+                   void* stream) {
     if (!io || n < 0 || !(out_dim == 1 || out_dim == 3)) return hipErrorInvalidValue;
+    if (compute != DD_MLP_F32 && compute != DD_MLP_F16X3) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
     if (!packed || !io->obs) return hipErrorInvalidValue;
     if (out_dim == 1 && (io->actions || io->log_prob)) return hipErrorInvalidValue;  // nothing to sample
     const dd::mlp::FwdArgs a{io->obs, io->out, io->actions, io->log_prob, io->seed, io->step, io->env_id_base, n};
-    return out_dim == 3 ? dd::mlp::launch<3>(packed, a, (hipStream_t)stream)
-                        : dd::mlp::launch<1>(packed, a, (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    if (compute == DD_MLP_F16X3)
+        return out_dim == 3 ? dd::mlp::launch<3, true>(packed, a, s) : dd::mlp::launch<1, true>(packed, a, s);
+    return out_dim == 3 ? dd::mlp::launch<3, false>(packed, a, s) : dd::mlp::launch<1, false>(packed, a, s);
 }
 
 }  // extern "C"

@@ -15,17 +15,18 @@ import torch  # noqa: F401  -- must be loaded first so the library binds torch's
 __all__ = [
     "DD_F32", "DD_F64", "DD_ACT_BITMASK", "DD_ACT_F32X3", "DD_ACT_U8X3", "DD_ACT_PHILOX",
     "DD_ST_DONE", "DD_ST_LANDED", "DD_ST_CRASHED", "DD_ST_PLAT_LEFT", "DD_OBS_DIM",
-    "DD_RENDER_HUD", "DD_RENDER_GAME_OVER",
+    "DD_RENDER_HUD", "DD_RENDER_GAME_OVER", "DD_MLP_F32", "DD_MLP_F16X3",
     "DDConfig", "DDState", "DDStepIO", "DDRolloutIO", "DDMlpParams", "DDMlpIO", "lib", "load", "library_path", "check",
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 5
+DD_ABI_VERSION = 6
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
 DD_OBS_DIM = 15
 DD_RENDER_HUD, DD_RENDER_GAME_OVER = 1, 2
+DD_MLP_F32, DD_MLP_F16X3 = 0, 1
 
 _D = ctypes.c_double
 _I = ctypes.c_int32
@@ -127,8 +128,8 @@ EXPORTS = {
     "dd_compact": (ctypes.c_int, [ctypes.c_void_p, _I, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "dd_mlp_packed_floats": (ctypes.c_int64, []),
-    "dd_mlp_pack": (ctypes.c_int, [ctypes.POINTER(DDMlpParams), ctypes.c_void_p, ctypes.c_void_p]),
-    "dd_mlp_forward": (ctypes.c_int, [ctypes.c_void_p, _I, ctypes.POINTER(DDMlpIO), ctypes.c_int64,
+    "dd_mlp_pack": (ctypes.c_int, [ctypes.POINTER(DDMlpParams), _I, ctypes.c_void_p, ctypes.c_void_p]),
+    "dd_mlp_forward": (ctypes.c_int, [ctypes.c_void_p, _I, _I, ctypes.POINTER(DDMlpIO), ctypes.c_int64,
                                       ctypes.c_void_p]),
     "dd_render": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, _I,

@@ -9,7 +9,10 @@ Actor_Critic_PPO.ipynb:376-424 share one body,
 with K = 3 + Sigmoid for the actor and K = 1 for the critic.  A
 :class:`MlpNet` takes that state_dict (the notebooks' ``.pth`` files load with
 ``torch.load(path, weights_only=True)``), packs it once into the kernel's
-MFMA operand order, and evaluates N observation rows per call in float32.
+MFMA operand order, and evaluates N observation rows per call in float32
+(``compute="f32"``, the default) or with the hidden GEMMs on the f16 MFMA as
+split hi/lo operand pairs (``compute="f16x3"``: about 4x faster, about the
+same end-to-end error; include/dronestep.h ``DD_MLP_F16X3``).
 The actor also does the collection loop's ``Bernoulli(probs).sample()`` and
 ``.log_prob(actions).sum(dim=1)`` (:857-859) in the same launch, returning the
 actions as the ``dd_step`` bitmask, so a policy-driven rollout never leaves
@@ -32,21 +35,27 @@ STATE_DICT_KEYS = ("0.weight", "0.bias", "1.weight", "1.bias", "3.weight", "3.bi
 _SHAPES = {"0.weight": (128, 15), "0.bias": (128,), "1.weight": (128,), "1.bias": (128,),
            "3.weight": (128, 128), "3.bias": (128,), "4.weight": (128,), "4.bias": (128,),
            "6.weight": (64, 128), "6.bias": (64,), "7.weight": (64,), "7.bias": (64,)}
+_COMPUTE = {"f32": abi.DD_MLP_F32, "f16x3": abi.DD_MLP_F16X3}
 
 
 class MlpNet:
     """Actor (``out_dim == 3``) or critic (``out_dim == 1``) on one GPU.
 
     ``state_dict`` keys may carry the notebooks' ``network.`` prefix or not.
-    ``ln_eps`` is nn.LayerNorm's default.  The packed parameters stay on
+    ``ln_eps`` is nn.LayerNorm's default.  ``compute`` is ``"f32"`` or
+    ``"f16x3"`` (see the module docstring).  The packed parameters stay on
     ``device``; ``library`` selects a build of libdronestep.so (tests, A/B).
     """
 
     def __init__(self, state_dict: Mapping[str, torch.Tensor], *, device="cuda", ln_eps: float = 1e-5,
-                 library=None):
+                 compute: str = "f32", library=None):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("MlpNet runs on the GPU (HIP); there is no CPU path")
+        if compute not in _COMPUTE:
+            raise ValueError(f"compute must be one of {sorted(_COMPUTE)}, got {compute!r}")
+        self.compute = compute
+        self._mode = _COMPUTE[compute]
         self._lib = library if library is not None else abi.lib()
         sd = {k[len("network."):] if k.startswith("network.") else k: v for k, v in state_dict.items()}
         missing = [k for k in STATE_DICT_KEYS if k not in sd]
@@ -65,7 +74,8 @@ class MlpNet:
                      for k in STATE_DICT_KEYS}
         p = abi.DDMlpParams(*[self._src[k].data_ptr() for k in STATE_DICT_KEYS], self.out_dim, self.ln_eps)
         self.packed = torch.empty(int(self._lib.dd_mlp_packed_floats()), dtype=torch.float32, device=self.device)
-        abi.check(self._lib.dd_mlp_pack(ctypes.byref(p), self.packed.data_ptr(), self._stream()), "dd_mlp_pack")
+        abi.check(self._lib.dd_mlp_pack(ctypes.byref(p), self._mode, self.packed.data_ptr(), self._stream()),
+                  "dd_mlp_pack")
 
     @classmethod
     def from_file(cls, path: str, **kw) -> "MlpNet":
@@ -87,8 +97,8 @@ class MlpNet:
                          actions.data_ptr() if actions is not None else None,
                          log_prob.data_ptr() if log_prob is not None else None,
                          int(seed) & (2 ** 64 - 1), int(step), int(env_id_base))
-        abi.check(self._lib.dd_mlp_forward(self.packed.data_ptr(), self.out_dim, ctypes.byref(io), obs.shape[0],
-                                           self._stream()), "dd_mlp_forward")
+        abi.check(self._lib.dd_mlp_forward(self.packed.data_ptr(), self._mode, self.out_dim, ctypes.byref(io),
+                                           obs.shape[0], self._stream()), "dd_mlp_forward")
 
     def __call__(self, obs: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``network(obs)``: probabilities ``[N, 3]`` (actor) or values ``[N]`` (critic)."""

@@ -1,10 +1,15 @@
-"""GPU: dd_mlp_forward (the notebooks' actor / critic on f32 MFMA) against the
-notebook models' own outputs (tests/golden/policy.npz) and a torch fp32
-reference, plus the Bernoulli sampling contract.
+"""GPU: dd_mlp_forward (the notebooks' actor / critic on f32 MFMA, and the
+opt-in f16x3 split-operand form) against the notebook models' own outputs
+(tests/golden/policy.npz) and a torch fp32 reference, plus the Bernoulli
+sampling contract.
 
-Tolerances (float32 model, different summation order than torch's):
-probabilities |d| <= 2e-6; values |d| <= 1e-5 * (1 + |v|) ... 2e-4 absolute at
-|v| ~ 600; log-probabilities |d| <= 1e-5 * (1 + |lp|)."""
+Tolerances (float32 model, different summation order than torch's), the same
+for both compute modes except the critic's values: probabilities |d| <= 2e-6;
+values |d| <= 1e-4 + 2e-6 |v| (f16x3: 4e-4 + 8e-6 |v|, VALUE_TOL);
+log-probabilities |d| <= 1e-5 * (1 + |lp|).  (f16x3 keeps ~22 bits per
+product, f32 accumulation: a numpy emulation on the fixture puts its actor
+probabilities within 5e-7 of float64, f32's within 4e-7:
+tools/mlp_split_sim.py.)"""
 import numpy as np
 import pytest
 import torch
@@ -28,24 +33,36 @@ def fixture():
     return gd.policy_fixture()
 
 
-def test_actor_probs_match_notebook_model(fixture, gpu_device):
+COMPUTE = ("f32", "f16x3")
+# critic values: the notebook critic's outputs reach |v| ~ 850 through a
+# Linear(64, 1) with large weights, which amplifies the hidden layers'
+# relative error; f16x3 keeps ~22 bits per product against f32's 24, so its
+# bound is 4x f32's (emulation: 2.0e-4 vs 1.3e-4 from float64 at worst).
+VALUE_TOL = {"f32": (2e-6, 1e-4), "f16x3": (8e-6, 4e-4)}
+
+
+@pytest.mark.parametrize("compute", COMPUTE)
+def test_actor_probs_match_notebook_model(fixture, gpu_device, compute):
     d, nets = fixture
-    actor = MlpNet(nets["actor"], device=gpu_device)
+    actor = MlpNet(nets["actor"], device=gpu_device, compute=compute)
     probs = actor(torch.as_tensor(d["obs"], device=gpu_device))
     close(probs.cpu().numpy(), d["probs"], 0.0, 2e-6)
 
 
-def test_critic_values_match_notebook_model(fixture, gpu_device):
+@pytest.mark.parametrize("compute", COMPUTE)
+def test_critic_values_match_notebook_model(fixture, gpu_device, compute):
     d, nets = fixture
-    critic = MlpNet(nets["critic"], device=gpu_device)
+    critic = MlpNet(nets["critic"], device=gpu_device, compute=compute)
     assert critic.out_dim == 1
     v = critic(torch.as_tensor(d["obs"], device=gpu_device))
-    close(v.cpu().numpy(), d["values"], 2e-6, 1e-4)
+    rel, abs_ = VALUE_TOL[compute]
+    close(v.cpu().numpy(), d["values"], rel, abs_)
 
 
-def test_log_prob_of_sampled_actions(fixture, gpu_device):
+@pytest.mark.parametrize("compute", COMPUTE)
+def test_log_prob_of_sampled_actions(fixture, gpu_device, compute):
     d, nets = fixture
-    actor = MlpNet(nets["actor"], device=gpu_device)
+    actor = MlpNet(nets["actor"], device=gpu_device, compute=compute)
     obs = torch.as_tensor(d["obs"], device=gpu_device)
     actions, lp, probs = actor.act(obs, seed=3, step=17, probs=True)
     bits = torch.stack([(actions >> j) & 1 for j in range(3)], dim=1).float()
@@ -89,15 +106,16 @@ def test_samples_are_keyed_by_env_and_step(fixture, gpu_device):
     assert not torch.equal(a, a3)
 
 
+@pytest.mark.parametrize("compute", COMPUTE)
 @pytest.mark.parametrize("n", [1, 31, 32, 33, 4097, 65_536 + 37])
-def test_random_weights_vs_torch_fp32(n, gpu_device):
+def test_random_weights_vs_torch_fp32(n, gpu_device, compute):
     """Freshly initialised networks (torch's default init) at ragged and
     config-5 sizes against torch on the same device."""
     torch.manual_seed(n)
     for k in (3, 1):
         sd = _random_sd(k)
         ref = gd.torch_mlp({kk: v.numpy() for kk, v in sd.items()}, device=gpu_device)
-        net = MlpNet(sd, device=gpu_device)
+        net = MlpNet(sd, device=gpu_device, compute=compute)
         obs = torch.randn(n, 15, device=gpu_device) * 2.0
         with torch.no_grad():
             want = ref(obs)
@@ -119,11 +137,12 @@ def _random_sd(k):
     return net.state_dict()
 
 
-def test_policy_driven_rollout_matches_host_loop(fixture, gpu_device):
+@pytest.mark.parametrize("compute", COMPUTE)
+def test_policy_driven_rollout_matches_host_loop(fixture, gpu_device, compute):
     """obs -> dd_mlp_forward (sample) -> dd_step for 40 frames, all on the
     device, equals the same loop with actions copied through the host."""
     d, nets = fixture
-    actor = MlpNet(nets["actor"], device=gpu_device)
+    actor = MlpNet(nets["actor"], device=gpu_device, compute=compute)
     a_env = VecDroneEnv(2048, device=gpu_device, randomize_drone=True, auto_reset=True, seed=4)
     b_env = VecDroneEnv(2048, device=gpu_device, randomize_drone=True, auto_reset=True, seed=4)
     oa, ob = a_env.reset(), b_env.reset()
@@ -146,3 +165,17 @@ def test_errors(fixture, gpu_device):
     bad["3.weight"] = bad["3.weight"][:, :64]
     with pytest.raises(ValueError):
         MlpNet(bad, device=gpu_device)
+    with pytest.raises(ValueError):
+        MlpNet(nets["actor"], device=gpu_device, compute="bf16")
+
+
+def test_f16x3_tracks_f32(fixture, gpu_device):
+    """The two compute modes agree with each other on the notebook model and
+    on observations far from the fixture's (|obs| up to ~40)."""
+    d, nets = fixture
+    a32 = MlpNet(nets["actor"], device=gpu_device)
+    a16 = MlpNet(nets["actor"], device=gpu_device, compute="f16x3")
+    torch.manual_seed(7)
+    obs = torch.cat([torch.as_tensor(d["obs"], device=gpu_device),
+                     torch.randn(4096, 15, device=gpu_device) * 10.0])
+    close(a16(obs).cpu().numpy(), a32(obs).cpu().numpy(), 0.0, 3e-6)

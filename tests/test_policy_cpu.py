@@ -38,8 +38,11 @@ def test_forward_argument_errors_without_gpu():
     lib = abi.lib()
     io = abi.DDMlpIO()
     import ctypes
-    assert lib.dd_mlp_forward(None, 2, ctypes.byref(io), 10, None) == 1   # bad out_dim
-    assert lib.dd_mlp_forward(None, 3, ctypes.byref(io), -1, None) == 1   # bad n
-    assert lib.dd_mlp_forward(None, 3, ctypes.byref(io), 0, None) == 0    # empty batch
-    assert lib.dd_mlp_forward(None, 3, ctypes.byref(io), 5, None) == 1    # null buffers
-    assert lib.dd_mlp_pack(None, None, None) == 1
+    for mode in (abi.DD_MLP_F32, abi.DD_MLP_F16X3):
+        assert lib.dd_mlp_forward(None, mode, 2, ctypes.byref(io), 10, None) == 1   # bad out_dim
+        assert lib.dd_mlp_forward(None, mode, 3, ctypes.byref(io), -1, None) == 1   # bad n
+        assert lib.dd_mlp_forward(None, mode, 3, ctypes.byref(io), 0, None) == 0    # empty batch
+        assert lib.dd_mlp_forward(None, mode, 3, ctypes.byref(io), 5, None) == 1    # null buffers
+        assert lib.dd_mlp_pack(None, mode, None, None) == 1
+    assert lib.dd_mlp_forward(None, 2, 3, ctypes.byref(io), 0, None) == 1           # bad compute
+    assert lib.dd_mlp_pack(None, 7, None, None) == 1

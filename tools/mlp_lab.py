@@ -22,6 +22,7 @@ def main():
     p.add_argument("--rows", default="65536,262144")
     p.add_argument("--rounds", type=int, default=15)
     p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--compute", default="f32", help="f32 or f16x3 (variants built before ABI 6 take f32 only)")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -32,7 +33,8 @@ def main():
         obs = torch.randn(n, 15, device=dev)
         acts = torch.empty(n, dtype=torch.uint8, device=dev)
         lp = torch.empty(n, device=dev)
-        nets = {v: (MlpNet(sd, device=dev, library=abi.load(os.path.join(LAB, f"lib_{v}.so"))), [])
+        nets = {v: (MlpNet(sd, device=dev, compute=args.compute,
+                           library=abi.load(os.path.join(LAB, f"lib_{v}.so"))), [])
                 for v in args.variants.split(",")}
         ref = None
         for v, (m, _) in nets.items():
@@ -57,7 +59,7 @@ def main():
                 ts.append(e0.elapsed_time(e1) * 1e3 / args.reps)
         for v, (m, ts) in nets.items():
             us = statistics.median(ts)
-            print(json.dumps({"rows": n, "variant": v, "us_median": round(us, 2), "us_min": round(min(ts), 2),
+            print(json.dumps({"rows": n, "variant": v, "compute": args.compute, "us_median": round(us, 2), "us_min": round(min(ts), 2),
                               "tflops": round(n * FLOPS / (us * 1e-6) / 1e12, 2)}), flush=True)
 
 

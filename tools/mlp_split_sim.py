@@ -1,0 +1,59 @@
+#!/usr/bin/env python
+"""numpy emulation of the DD_MLP_F16X3 split-operand GEMMs on the notebook models
+(tests/golden/policy.npz): max probability / value error against float64, next
+to plain float32.  Operands split as a = hi + lo * 2^-11 with hi, lo f16
+(both rounded to nearest-even: truncating them, v_cvt_pkrtz, biases lo and
+quadruples the error; run with --truncate), products exact, sums rounded to f32."""
+import sys
+
+import numpy as np
+
+TRUNCATE = '--truncate' in sys.argv
+d = np.load(__import__('os').path.join(__import__('os').path.dirname(__import__('os').path.abspath(__file__)), '..', 'tests', 'golden', 'policy.npz'))
+def rtz16(x):
+    """float32 -> float16 rounded toward zero (v_cvt_pkrtz_f16_f32)."""
+    h = x.astype(np.float16)
+    over = np.abs(h.astype(np.float32)) > np.abs(x)
+    return np.where(over, np.nextafter(h, np.float16(0)), h)
+
+
+def split(a):
+    a = a.astype(np.float32)
+    hi = a.astype(np.float16)  # v_cvt_pk_f16_f32, nearest-even; a - hi is exact
+    lo = ((a - hi.astype(np.float32)) * np.float32(2048)).astype(np.float16)
+    if TRUNCATE:  # the v_cvt_pkrtz_f16_f32 form, for comparison
+        hi = rtz16(a)
+        lo = rtz16((a - hi.astype(np.float32)) * np.float32(2048))
+    return hi, lo
+def lin(W, x, b, mode):
+    # W [o,i], x [n,i]
+    if mode == 'f64':
+        return x.astype(np.float64) @ W.T.astype(np.float64) + b
+    if mode == 'f32':
+        return (x.astype(np.float32) @ W.T.astype(np.float32) + b).astype(np.float32)
+    Wh, Wl = split(W); xh, xl = split(x)
+    f = lambda a: a.astype(np.float64)
+    main = f(xh) @ f(Wh).T
+    cross = (f(xh) @ f(Wl).T + f(xl) @ f(Wh).T)
+    # emulate f32 accumulation coarsely: round each sum to f32
+    return (main.astype(np.float32) + (cross.astype(np.float32) * np.float32(2**-11))).astype(np.float32) + b
+def ln(x, w, b, mode):
+    dt = np.float64 if mode == 'f64' else np.float32
+    x = x.astype(dt); m = x.mean(1, keepdims=True); v = ((x - m) ** 2).mean(1, keepdims=True)
+    return np.maximum((x - m) / np.sqrt(v + 1e-5) * w + b, 0)
+def fwd(pre, mode):
+    x = d['obs']
+    for i, j in ((0, 1), (3, 4), (6, 7)):
+        x = lin(d[f'{pre}.network.{i}.weight'], x, d[f'{pre}.network.{i}.bias'], mode)
+        x = ln(x, d[f'{pre}.network.{j}.weight'], d[f'{pre}.network.{j}.bias'], mode)
+    z = lin(d[f'{pre}.network.9.weight'], x, d[f'{pre}.network.9.bias'], 'f64' if mode == 'f64' else 'f32')
+    return z
+for pre in ('actor', 'critic'):
+    ref = fwd(pre, 'f64')
+    for mode in ('f32', 'split'):
+        z = fwd(pre, mode)
+        if pre == 'actor':
+            p = 1/(1+np.exp(-z.astype(np.float64))); pr = 1/(1+np.exp(-ref))
+            print(pre, mode, 'max |dprob| vs f64', np.abs(p - pr).max(), 'vs golden', np.abs(p - d['probs']).max())
+        else:
+            print(pre, mode, 'max |dv| vs f64', np.abs(z[:,0]-ref[:,0]).max(), 'vs golden', np.abs(z[:,0]-d['values']).max(), 'max|v|', np.abs(ref).max())

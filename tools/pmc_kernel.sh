@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU box: SQ counters of one kernel family (tools/prof_driver.py --what W),
 # one rocprofv3 pass per counter group, then a per-wave summary.
-#   WHAT=rollout|step  ENVS=...  REGEX=kernel-name regex  LIB=alt .so (optional)
+#   WHAT=rollout|step|mlp  ENVS=...  REGEX=kernel-name regex  LIB=alt .so (optional)
+#   COMPUTE=f32|f16x3 (mlp)  EXTRA_GROUPS="A B;C D" more counter passes
 set -o pipefail
 OUT=gpurun_out/${1:-pmc_kernel}
 WHAT=${WHAT:-rollout}; ENVS=${ENVS:-65536}; REGEX=${REGEX:-rollout_kernel}
@@ -17,6 +18,7 @@ groups=(
 )
 [ -n "$EXTRA_GROUPS" ] && IFS=';' read -ra xg <<< "$EXTRA_GROUPS" && groups+=("${xg[@]}")
 LIBARG=""; [ -n "$LIB" ] && LIBARG="--lib $LIB"
+[ -n "$COMPUTE" ] && LIBARG="$LIBARG --compute $COMPUTE"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace -f csv -- python3 tools/prof_driver.py --what $WHAT --envs $ENVS $LIBARG > /dev/null 2>> $OUT/err.log || { echo "trace failed"; exit 1; }
 i=0
 for g in "${groups[@]}"; do

@@ -18,6 +18,7 @@ def main():
     p.add_argument("--frames", type=int, default=256)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--lib", default="")
+    p.add_argument("--compute", default="f32", help="mlp: f32 or f16x3")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     lib = abi.load(args.lib) if args.lib else None
@@ -41,6 +42,7 @@ def main():
                             nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(),
                             nn.Linear(64, 3))
         kw2 = {"library": lib} if lib is not None else {}
+        kw2["compute"] = args.compute
         actor = MlpNet(net.state_dict(), device=dev, **kw2)
         o = torch.randn(n, 15, device=dev)
         acts_out = torch.empty(n, dtype=torch.uint8, device=dev)
