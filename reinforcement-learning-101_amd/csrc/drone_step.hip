@@ -496,7 +496,15 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <int P, typename E>
 __device__ __forceinline__ void store_as(E* base, uint32_t i, E v) {
-    if constexpr (P == kPlain) {
+    if constexpr (P >= 100) {  // lab sweeps: a raw buffer store with cache-policy bits P - 100
+        const uint32_t off = i * (uint32_t)sizeof(E);
+        if constexpr (sizeof(E) == 1)
+            __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), rsrc_of(base), off, 0, P - 100);
+        else if constexpr (sizeof(E) == 4)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rsrc_of(base), off, 0, P - 100);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsrc_of(base), off, 0, P - 100);
+    } else if constexpr (P == kPlain) {
         at(base, i) = v;
     } else if constexpr (P == kNT) {
         __builtin_nontemporal_store(v, &at(base, i));
@@ -518,7 +526,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // One 16-byte observation store at float4 index k of a wave-uniform base.
 template <int P>
 __device__ __forceinline__ void store_obs4(f32x4* base, uint32_t k, f32x4 v) {
-    if constexpr (P == kPlain) {
+    if constexpr (P >= 100) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base), k * 16u, 0, P - 100);
+    } else if constexpr (P == kPlain) {
         at(base, k) = v;
     } else if constexpr (P == kNT) {
         __builtin_nontemporal_store(v, &at(base, k));
@@ -766,11 +776,27 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     return ended;
 }
 
+#ifdef DD_EXP_TIMELINE
+// Lab-only (tools/timeline_lab.py): per wave, the 100 MHz real-time clock at
+// kernel entry, loads complete, frame done, obs issued and stores complete,
+// the shader-clock entry/exit, and HW_ID / XCC_ID, for the last launch.
+constexpr int kTlWaves = 1 << 14;
+__device__ uint64_t dd_tl_buf[kTlWaves * 8];
+#define DD_TL(k) tl[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define DD_TL(k) (void)0
+#endif
+
 // dd_step kernel: one drone per lane, one tile of kStepBlock lanes per block.
 template <typename T, int AFMT, bool kRef, bool kShaped>
 __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
 #ifdef DD_EXP_EMPTY  // timing-only: the launch and dispatch floor
     if (p.n >= 0) return;
+#endif
+#ifdef DD_EXP_TIMELINE
+    uint64_t tl[8];
+    tl[5] = __builtin_amdgcn_s_memtime();
+    DD_TL(0);
 #endif
     __shared__ __attribute__((aligned(16))) float tile[kStepBlock * DD_OBS_DIM];
     const uint32_t row0 = blockIdx.x * kStepBlock;
@@ -782,7 +808,12 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
                  "s"(a.px), "s"(a.py), "s"(a.total), "s"(a.status), "s"(a.steps), "s"(p.actions));
     Raw<T> r;
     if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r);
+#ifdef DD_EXP_TIMELINE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DD_TL(1);
+#endif
     const bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM);
+    DD_TL(2);
     if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
         const uint64_t m = __ballot(ended);
         if (m) {
@@ -801,6 +832,19 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
         const int rows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
         flush_obs_wave(tile + (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM, p.obs + (size_t)wrow0 * DD_OBS_DIM, rows);
     }
+#ifdef DD_EXP_TIMELINE
+    DD_TL(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DD_TL(4);
+    tl[6] = __builtin_amdgcn_s_memtime();
+    tl[7] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+            ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);  // HW_ID, XCC_ID
+    const uint32_t w = (blockIdx.x * kStepBlock + threadIdx.x) / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0 && w < (uint32_t)kTlWaves) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dd_tl_buf[w * 8 + k] = tl[k];
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1540,5 +1584,14 @@ int64_t dd_step_bytes_per_env(int32_t precision, int32_t action_format, int32_t 
 const char* dd_error_string(int code) { return hipGetErrorString((hipError_t)code); }
 
 int dd_abi_version(void) { return DD_ABI_VERSION; }
+
+#ifdef DD_EXP_TIMELINE
+// Lab-only: copies the last step launch's per-wave timeline (8 x u64 per wave).
+int dd_lab_timeline(void* dst, int64_t bytes) {
+    const int64_t cap = (int64_t)sizeof(uint64_t) * 8 * dd::kTlWaves;
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(dd::dd_tl_buf), (size_t)(bytes < cap ? bytes : cap), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // extern "C"
