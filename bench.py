@@ -449,6 +449,43 @@ def policy_rollout_point(n, frames, seed, dev, compute="f32"):
             "launch": f"hipGraph of {frames} x (dd_mlp_forward + dd_step)"}
 
 
+def policy_fused_point(n, frames, seed, dev, compute="f16x3", reps=5):
+    """collect_episodes_ppo with the actor in the loop as ONE launch
+    (dd_policy_rollout, VecDroneEnv.policy_rollout): per frame the actor,
+    Bernoulli sampling and the frame, writing the PPO buffers obs [T, N, 15],
+    actions, log-probs, rewards and dones.  env-steps/s with the policy's
+    inference included; same work as policy_rollout_point plus the per-frame
+    buffers that point does not keep."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv
+    actor = _random_actor(dev, seed, compute)
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg)
+    env.reset()
+    bufs = dict(obs_out=torch.empty(frames, n, 15, device=dev),
+                actions_out=torch.empty(frames, n, dtype=torch.uint8, device=dev),
+                log_prob_out=torch.empty(frames, n, device=dev), reward_out=torch.empty(frames, n, device=dev),
+                done_out=torch.empty(frames, n, dtype=torch.bool, device=dev))
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        env.policy_rollout(actor, frames, seed=seed, **bufs)  # warm-up (and LDS attribute set-up)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for r in range(reps):
+            env.policy_rollout(actor, frames, seed=seed, step=(r + 1) * frames, **bufs)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    tfs = n * frames * MLP_FLOPS_PER_ROW / (ms * 1e-3) / 1e12
+    del actor, env, bufs
+    torch.cuda.empty_cache()
+    return {"envs": n, "frames": frames, "compute": compute, "ms": round(ms, 3),
+            "steps_per_s": round(n * frames / (ms * 1e-3), 1), "us_per_frame": round(ms * 1e3 / frames, 2),
+            "actor_tflops": round(tfs, 2), "launch": f"one dd_policy_rollout launch per {frames} frames",
+            "kernel": f"dd::prl::policy_rollout_kernel<float, {'true' if compute == 'f16x3' else 'false'}, true>"}
+
+
 def render_point(seed, dev, frames=64, reps=20):
     """DroneGame.render('rgb_array') as dd_render, `frames`
     lanes of a running batch per launch (HUD and game-over overlay on).
@@ -639,7 +676,7 @@ def main():
             gp = gather_point(env, n, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
             gp = {"error": f"{type(e).__name__}: {e}"[:300]}
-    c5 = c5a = g5 = c2 = nb = pp = pr = pp16 = pr16 = sp = rp = None
+    c5 = c5a = g5 = c2 = nb = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         c5a = step_loop_point(args.rollout_point, 256, args.precision, args.seed, dev)
@@ -651,6 +688,8 @@ def main():
         pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
         pp16 = policy_point(args.rollout_point or 65_536, args.seed, dev, "f16x3")
         pr16 = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev, "f16x3")
+        pf = policy_fused_point(args.rollout_point or 65_536, 64, args.seed, dev, "f32")
+        pf16 = policy_fused_point(args.rollout_point or 65_536, 64, args.seed, dev, "f16x3")
         sp = socket_point(args.seed, dev)
         rp = render_point(args.seed, dev)
 
@@ -710,6 +749,8 @@ def main():
             "policy_rollout_point": pr,
             "policy_point_f16x3": pp16,
             "policy_rollout_point_f16x3": pr16,
+            "policy_fused_point": pf,
+            "policy_fused_point_f16x3": pf16,
             "socket_point": sp,
             "render_point": rp,
             "gpu_ms_per_step": round(step_ms, 6),

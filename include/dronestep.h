@@ -18,6 +18,8 @@
  *   DroneGamerBoi / DroneTeacherBoi + Bernoulli.sample / log_prob
  *                             Actor_Critic_PPO.ipynb:376-424, :851-859 -> dd_mlp_forward
  *   compute_gae               Actor_Critic_PPO.ipynb:733-787          -> dd_gae
+ *   collect_episodes_ppo with the actor in the loop
+ *                             Actor_Critic_PPO.ipynb:797-917          -> dd_policy_rollout
  *
  * One call processes a batch of N independent drones stored as a
  * struct-of-arrays (SoA) in device memory.  The reference has no FFI of its
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 6
+#define DD_ABI_VERSION 7
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -305,6 +307,41 @@ int dd_mlp_pack(const DDMlpParams *params, int32_t compute, float *packed, void 
 /* Forward pass; out_dim and compute must match the packed parameters. */
 int dd_mlp_forward(const float *packed, int32_t compute, int32_t out_dim,
                    const DDMlpIO *io, int64_t n, void *stream);
+
+/* ---- The collection loop with the actor in it --
+ * collect_episodes_ppo (Actor_Critic_PPO.ipynb:797-917) for N drones and
+ * `frames` frames in one launch: per frame, the actor on the current
+ * observation (dd_mlp_forward's network and sampling, :851-859), then the
+ * drone frame (dd_step) with the sampled action.  Frame k writes
+ *   obs[k]      the policy input (the observation before the frame; frame 0's
+ *               is obs0, later ones are the previous frame's dd_step obs)
+ *   actions[k], log_prob[k]   as dd_mlp_forward with step = step + k
+ *   reward[k], done[k]        as dd_step (reward_mode as DDRolloutIO)
+ * and obs_final receives the observation after the last frame.  Equal, bit
+ * for bit, to `frames` x (dd_mlp_forward(obs) ; dd_step(actions)) with the
+ * state's env ids as the sampling ids.  The actor's packed parameters
+ * (dd_mlp_pack, out_dim 3) are read into LDS once per launch. */
+typedef struct DDPolicyRolloutIO {
+    const float *obs0;    /* [N][15] observation before frame 0 (required)      */
+    float *obs_final;     /* [N][15] observation after the last frame (nullable;
+                             may be obs0)                                        */
+    float *obs;           /* [frames][N][15] policy inputs (nullable)           */
+    uint8_t *actions;     /* [frames][N] sampled bitmask (nullable)             */
+    float *log_prob;      /* [frames][N] summed log-probability (nullable)      */
+    void *reward;         /* float or double [frames][N] by precision (required) */
+    uint8_t *done;        /* uint8 [frames][N] (required)                       */
+    uint64_t seed;        /* Bernoulli draws: Philox4x32-10 key                 */
+    int64_t step;         /* sampling step of frame 0 (frame k: step + k)       */
+    int32_t frames;
+    int32_t max_steps;    /* notebook mode: episode cap, <= 0 = none            */
+    double *shaped_hist;  /* notebook reward mode, as DDRolloutIO (nullable)    */
+    void *engine_reward;  /* notebook mode: the engine's reward / done          */
+    uint8_t *engine_done; /* [frames][N] (both or neither, nullable)            */
+} DDPolicyRolloutIO;
+
+int dd_policy_rollout(const DDConfig *cfg, const DDState *st, const float *packed,
+                      int32_t compute, const DDPolicyRolloutIO *io, int64_t n,
+                      void *stream);
 
 /* ---- Rendering -------------------------------------
  * DroneGame.render() in 'rgb_array' mode (game_engine.py:300-337): the scene

@@ -1,0 +1,471 @@
+// frame.h — one drone's frame of DroneGame.step in IEEE double: world
+// constants, the lane state, Drone.apply_thrust / update, the reward cascade,
+// get_state's observation row and the notebooks' calc_reward.  Shared by the
+// step / rollout kernels (drone_step.hip) and the fused policy rollout
+// (policy_rollout.hip), so every path evaluates the same frame bit for bit.
+// Compiled with -ffp-contract=off (see drone_step.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <type_traits>
+
+#include "dronestep.h"
+#include "philox.h"
+#include "trig.h"
+
+namespace dd {
+
+// numpy's deg2rad: x * (NPY_PI / 180.0)   (physics.py:16, np.radians)
+constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
+
+// sin and cos of an angle in degrees, as rotate_point computes them
+// (physics.py:16-18).  DD_TRIG_OCML selects the ROCm device library's
+// general-argument sincos instead of trig.h's (timing experiments).
+__device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
+#if defined(DD_EXP_FAKE_TRIG)  // timing-only sensitivity: what the trig costs
+    *s = deg * 1e-3;
+    *c = 1.0 - fabs(*s);
+#elif defined(DD_TRIG_OCML)
+    ::sincos(deg * kDeg2Rad, s, c);
+#else
+    trig::sincos(deg * kDeg2Rad, s, c);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// World constants
+// ---------------------------------------------------------------------------
+// config.py:17-68 as a DDConfig (also what dd_config_default returns).
+constexpr DDConfig reference_config() {
+    DDConfig c{};
+    c.gravity = 0.3;
+    c.drag = 0.99;
+    c.angular_drag = 0.95;
+    c.main_thrust_power = 0.6;
+    c.side_thrust_power = 0.3;
+    c.fuel_main = 2.0;
+    c.fuel_side = 1.0;
+    c.max_fuel = 1000.0;
+    c.drone_half_height = 20 / 2.0;
+    c.dt = 1.0;
+    c.platform_half_width = 100 / 2.0;
+    c.platform_half_height = 20 / 2.0;
+    c.platform_speed = 1.0;
+    c.platform_min_x = 100 / 2;
+    c.platform_max_x = 800 - 100 / 2;
+    c.max_landing_velocity = 3.0;
+    c.max_landing_angle = 20.0;
+    c.world_width = 800;
+    c.world_height = 600;
+    c.oob_margin = 50;
+    c.ground_level = 600 - 50;
+    c.wind_x = 0.0;
+    c.wind_y = 0.0;
+    c.reward_step = -0.1;
+    c.reward_landing = 100.0;
+    c.reward_crash = -100.0;
+    c.reward_out_of_fuel = -50.0;
+    c.reward_out_of_bounds = -50.0;
+    c.shaping_offset = 500;
+    c.shaping_scale = 5000;
+    c.vel_scale = 10.0;
+    c.angle_scale = 180.0;
+    c.drone_start_x = 800 / 2;
+    c.drone_start_y = 100;
+    c.drone_x_min = 100;
+    c.drone_x_max = 700;
+    c.drone_y_min = 50;
+    c.drone_y_max = 250;
+    c.platform_start_x = 800 / 2;
+    c.platform_start_y = 600 - 100;
+    c.platform_x_lo = 100 / 2 + 50;
+    c.platform_x_hi = 800 - 100 / 2 - 50;
+    c.platform_y_lo = 100;
+    c.platform_y_hi = 550;
+    c.wind_enabled = 0;
+    c.platform_moving = 0;
+    c.randomize_drone = 0;
+    c.randomize_platform = 1;
+    c.auto_reset = 0;
+    c.seed = 0;
+    return c;
+}
+
+// The constants the frame reads: the config plus the correctly rounded
+// reciprocals of its divisors (for trig::div_exact).
+struct Consts {
+    DDConfig c;
+    double inv_w, inv_h, inv_vel, inv_angle, inv_fuel, inv_shaping;
+};
+
+constexpr Consts make_consts(const DDConfig& c) {
+    Consts k{};
+    k.c = c;
+    k.inv_w = 1.0 / c.world_width;
+    k.inv_h = 1.0 / c.world_height;
+    k.inv_vel = 1.0 / c.vel_scale;
+    k.inv_angle = 1.0 / c.angle_scale;
+    k.inv_fuel = 1.0 / c.max_fuel;
+    k.inv_shaping = 1.0 / c.shaping_scale;
+    return k;
+}
+
+// The reference's physics, reward and observation constants as compile-time
+// data: kernels instantiated with kRef = true read them from here and the
+// compiler folds them into the instruction stream (no kernarg SGPRs, no SGPR
+// spills).  Switches, spawn ranges, wind and seed always come from the call.
+__device__ constexpr Consts kRefConsts = make_consts(reference_config());
+
+// True when every double the frame reads (wind aside) equals config.py's
+// and the run has neither wind nor a moving platform: the kernels' kRef
+// instantiation, whose frame compiles neither in.
+inline bool uses_reference_physics(const DDConfig& c) {
+    if (c.wind_enabled || c.platform_moving) return false;
+    const DDConfig r = reference_config();
+    const double* a = &c.gravity;
+    const double* b = &r.gravity;
+    const int n = (int)((&c.vel_scale - &c.gravity) + 1);
+    for (int j = 0; j < n; ++j) {
+        if (a + j == &c.wind_x || a + j == &c.wind_y) continue;
+        if (memcmp(a + j, b + j, sizeof(double)) != 0) return false;
+    }
+    return true;
+}
+
+// Uniform integer in [lo, lo + span) from one 32-bit draw (multiply-high).
+__device__ __forceinline__ int32_t draw_range(uint32_t r, int32_t lo, uint32_t span) {
+    return lo + (int32_t)(((uint64_t)r * span) >> 32);
+}
+
+// ---------------------------------------------------------------------------
+// One drone
+// ---------------------------------------------------------------------------
+// The per-lane state, widened to double for the frame's arithmetic.
+struct Lane {
+    double x, y, vx, vy, angle, omega, fuel, px, py, total;
+    double speed, dist;  // derived: Drone.get_speed, physics.distance to the pad
+    uint32_t status;
+    int32_t steps, episode;
+};
+
+// Drone.get_speed (drone.py:139-145) and physics.distance (physics.py:42-44)
+// of the current state; both the reward and get_state use them.
+__device__ __forceinline__ void measure(Lane& s) {
+    const double dx = s.px - s.x, dy = s.py - s.y;
+#ifdef DD_EXP_FAKE_SQRT  // timing-only sensitivity: what the two square roots cost
+    s.speed = (s.vx * s.vx + s.vy * s.vy) * 0.25;
+    s.dist = (dx * dx + dy * dy) * 0.001;
+#else
+    s.speed = sqrt(s.vx * s.vx + s.vy * s.vy);
+    s.dist = sqrt(dx * dx + dy * dy);
+#endif
+}
+
+// DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
+// Platform.reset (platform.py:104-114).  `c` is the call's config (switches,
+// spawn ranges, seed), `max_fuel` the physics' (compile-time under kRef, so
+// a rollout's frame loop issues no scalar load that a join's lgkmcnt wait
+// would couple to its LDS reads); s.episode becomes the value after
+// `episode += 1`.
+__device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_t env, Lane& s) {
+    s.episode += 1;
+    uint32_t r[4];
+    philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)s.episode, 0u,
+                  (uint32_t)c.seed, (uint32_t)(c.seed >> 32), r);
+    if (c.randomize_drone) {
+        s.x = draw_range(r[0], c.drone_x_min, (uint32_t)(c.drone_x_max - c.drone_x_min + 1));
+        s.y = draw_range(r[1], c.drone_y_min, (uint32_t)(c.drone_y_max - c.drone_y_min + 1));
+    } else {
+        s.x = c.drone_start_x;
+        s.y = c.drone_start_y;
+    }
+    if (c.randomize_platform) {
+        s.px = draw_range(r[2], c.platform_x_lo, (uint32_t)(c.platform_x_hi - c.platform_x_lo));
+        s.py = draw_range(r[3], c.platform_y_lo, (uint32_t)(c.platform_y_hi - c.platform_y_lo));
+    } else {
+        s.px = c.platform_start_x;
+        s.py = c.platform_start_y;
+    }
+    s.vx = 0.0; s.vy = 0.0; s.angle = 0.0; s.omega = 0.0;
+    s.fuel = max_fuel;
+    s.status = 0u;  // not done / landed / crashed; platform direction +1
+    s.steps = 0;
+    s.total = 0.0;
+    measure(s);
+}
+
+// physics.normalize_angle after one frame's turn.  |omega| stays near
+// 0.3 / (1 - 0.95) = 6 degrees per frame, so the angle leaves (-540, 540]
+// only if the caller wrote such an angle; then the loop form runs (a rare,
+// separate branch).  One exact +-360 equals the reference's while-loops
+// inside that range (NaN passes through both unchanged).
+__device__ __forceinline__ double wrap_angle(double a) {
+    double w = a > 180.0 ? a - 360.0 : a;
+    w = a < -180.0 ? a + 360.0 : w;
+    if (__builtin_expect(fabs(a) > 540.0, 0)) w = trig::normalize_angle(a);
+    return w;
+}
+
+// One frame of a live lane: Drone.apply_thrust (drone.py:44-76), wind
+// (game_engine.py:121-123), Drone.update (drone.py:78-103), Platform.update
+// (platform.py:31-49), _calculate_reward with _check_landing / _check_crash /
+// _check_out_of_bounds (game_engine.py:179-279).  `k` holds the physics
+// (compile-time under kRef), `sw` the call's switches; kRef also means no
+// wind and a static platform (their code is not compiled in).  Returns the
+// reward.
+//
+// kFlat (the rollout kernel, one wave per SIMD at its usual size): the
+// common path is one basic block.  The thrusters are applied through
+// selects (the thrust vector's sincos runs for every lane; a wave almost
+// always has a lane firing its main engine anyway) and the angle wrap is a
+// select with a rare fallback, so the scheduler can interleave the frame's
+// independent chains (sincos, fuel and spin, the two square roots) where
+// no other wave fills the stalls: 65,536 x 256 frames 0.424 -> 0.403 ms.
+// The step kernel (four waves per SIMD) keeps the branches: selects cost it
+// VALU slots the other waves would use.  Only the bottom-centre test near
+// the pad (rare) branches in both.
+template <bool kRef, bool kFlat>
+__device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
+    const DDConfig& c = k.c;
+
+    // apply_thrust: each thruster gated on fuel > 0 at that moment, in order
+    const double ty = -c.main_thrust_power;
+    if constexpr (kFlat) {
+        const bool main_on = (act & 1u) && s.fuel > 0.0;
+        double sa, ca;
+        sincos_deg(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
+        s.vx = main_on ? s.vx + (0.0 * ca - ty * sa) : s.vx;
+        s.vy = main_on ? s.vy + (0.0 * sa + ty * ca) : s.vy;
+        s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
+        const bool left_on = (act & 2u) && s.fuel > 0.0;
+        s.omega = left_on ? s.omega - c.side_thrust_power : s.omega;
+        s.fuel = left_on ? s.fuel - c.fuel_side : s.fuel;
+        const bool right_on = (act & 4u) && s.fuel > 0.0;
+        s.omega = right_on ? s.omega + c.side_thrust_power : s.omega;
+        s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
+    } else {
+        if ((act & 1u) && s.fuel > 0.0) {
+            double sa, ca;
+            sincos_deg(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)
+            s.vx += 0.0 * ca - ty * sa;
+            s.vy += 0.0 * sa + ty * ca;
+            s.fuel -= c.fuel_main;
+        }
+        if ((act & 2u) && s.fuel > 0.0) { s.omega -= c.side_thrust_power; s.fuel -= c.fuel_side; }
+        if ((act & 4u) && s.fuel > 0.0) { s.omega += c.side_thrust_power; s.fuel -= c.fuel_side; }
+    }
+    s.fuel = s.fuel > 0.0 ? s.fuel : 0.0;  // max(0, fuel)
+
+    if (!kRef && sw.wind_enabled) { s.vx += sw.wind_x; s.vy += sw.wind_y; }
+
+    s.vy += c.gravity * c.dt;
+    s.vx *= c.drag;
+    s.vy *= c.drag;
+    s.x += s.vx * c.dt;
+    s.y += s.vy * c.dt;
+    s.angle += s.omega * c.dt;
+    s.omega *= c.angular_drag;
+#ifdef DD_EXP_STEP_WRAP_SELECT
+    s.angle = wrap_angle(s.angle);
+#else
+    s.angle = kFlat ? wrap_angle(s.angle) : trig::normalize_angle(s.angle);
+#endif
+
+    if (!kRef && sw.platform_moving) {
+        const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
+        s.px += c.platform_speed * dir * c.dt;
+        if (s.px <= c.platform_min_x) { s.px = c.platform_min_x; s.status &= ~DD_ST_PLAT_LEFT; }
+        else if (s.px >= c.platform_max_x) { s.px = c.platform_max_x; s.status |= DD_ST_PLAT_LEFT; }
+    }
+
+    measure(s);  // speed (get_speed) and distance (physics.distance), shared with get_state
+    const bool slow = !(s.speed > c.max_landing_velocity);
+    const bool upright = fabs(s.angle) <= c.max_landing_angle;
+
+    // get_bottom_center: rotate_point(0, height / 2, angle) on the updated
+    // angle.  It only matters through on_pad, and the bottom centre lies
+    // within |half_height| (+ rounding) of (x, y), so the rotation (the
+    // frame's second sincos) runs only for slow, upright drones within that
+    // reach of the pad; every other lane has on_pad = false exactly as the
+    // reference's comparisons would give (NaN fails both tests alike).
+    bool on_pad = false;
+    const double rx = c.platform_half_width + fabs(c.drone_half_height);
+    const double ry = c.platform_half_height + fabs(c.drone_half_height);
+    const double slack = 1.0 + 1e-9 * (fabs(s.x) + fabs(s.y) + fabs(s.px) + fabs(s.py) + rx + ry);
+    if (slow && upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack) {
+        double sb, cb;
+        sincos_deg(s.angle, &sb, &cb);
+        const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
+        const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
+        on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
+                 (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
+    }
+
+    // _calculate_reward's cascade, evaluated branch-free: every predicate is
+    // formed, then the first that holds picks the term.  (The nested
+    // else-if form miscompiled on ROCm 7.2 / gfx950: the divergent-branch phi
+    // register of the out-of-bounds term was reused as a temporary, giving
+    // 649.9 instead of -50.1; tests/test_gpu_parity.py pins every branch.)
+    const bool landing = on_pad & slow & upright;                         // _check_landing
+    const bool crash = s.y > c.ground_level;                              // _check_crash, landing ruled out
+    const bool no_fuel = s.fuel <= 0.0;
+    const bool oob = (s.x < -c.oob_margin) | (s.x > c.world_width + c.oob_margin) |
+                     (s.y < -c.oob_margin) | (s.y > c.world_height + c.oob_margin);
+    double term = trig::div_exact(c.shaping_offset - s.dist, c.shaping_scale, k.inv_shaping);
+    const bool terminal = landing | crash | no_fuel | oob;
+    if constexpr (kRef) {
+        // config.py's terminal rewards are integers: pick one as an int (one
+        // literal per select) and widen it once, instead of selecting doubles
+        // (two literal moves and two selects each): dd_rollout 65,536 x 256
+        // 0.372 -> 0.365 ms, 262,144 x 256 0.952 -> 0.928 ms
+        constexpr DDConfig r = reference_config();
+        static_assert(r.reward_landing == 100.0 && r.reward_crash == -100.0 && r.reward_out_of_fuel == -50.0 &&
+                      r.reward_out_of_bounds == -50.0, "integer terminal rewards");
+        const int32_t ti = landing ? 100 : crash ? -100 : -50;
+        term = terminal ? (double)ti : term;
+    } else {
+        term = oob ? c.reward_out_of_bounds : term;
+        term = no_fuel ? c.reward_out_of_fuel : term;
+        term = crash ? c.reward_crash : term;
+        term = landing ? c.reward_landing : term;
+    }
+    s.status |= landing ? (DD_ST_LANDED | DD_ST_DONE) : terminal ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
+    const double reward = c.reward_step + term;
+    s.total += reward;
+    s.steps += 1;
+    return reward;
+}
+
+// DroneGame.get_state (game_engine.py:140-177) in state_to_array order, as the
+// reference's doubles (columns 0-12; 13/14 are the landed / crashed flags);
+// measure() has run on `s`.
+template <bool kGuard = false>
+__device__ __forceinline__ void observe_values(const Consts& k, const Lane& s, double v[13]) {
+    const DDConfig& c = k.c;
+    const double dx = s.px - s.x, dy = s.py - s.y;
+#ifdef DD_OBS_MUL  // experiment: x * RN(1/d), one op per column instead of three
+#define DD_Q(x, d, inv) ((x) * (inv))
+#else
+#define DD_Q(x, d, inv) (kGuard ? trig::div_exact_guarded((x), (d), (inv)) : trig::div_exact((x), (d), (inv)))
+#endif
+    v[0] = DD_Q(s.x, c.world_width, k.inv_w);
+    v[1] = DD_Q(s.y, c.world_height, k.inv_h);
+    v[2] = DD_Q(s.vx, c.vel_scale, k.inv_vel);
+    v[3] = DD_Q(s.vy, c.vel_scale, k.inv_vel);
+    v[4] = DD_Q(s.angle, c.angle_scale, k.inv_angle);
+    v[5] = DD_Q(s.omega, c.vel_scale, k.inv_vel);
+    v[6] = DD_Q(s.fuel, c.max_fuel, k.inv_fuel);
+    v[7] = DD_Q(s.px, c.world_width, k.inv_w);
+    v[8] = DD_Q(s.py, c.world_height, k.inv_h);
+    v[9] = DD_Q(s.dist, c.world_width, k.inv_w);
+    v[10] = DD_Q(dx, c.world_width, k.inv_w);
+    v[11] = DD_Q(dy, c.world_height, k.inv_h);
+    v[12] = DD_Q(s.speed, c.vel_scale, k.inv_vel);
+#undef DD_Q
+}
+
+__device__ __forceinline__ void write_obs_row(const double v[13], uint32_t status, float* o) {
+#pragma unroll
+    for (int j = 0; j < 13; ++j) o[j] = (float)v[j];
+    o[13] = (status & DD_ST_LANDED) ? 1.0f : 0.0f;
+    o[14] = (status & DD_ST_CRASHED) ? 1.0f : 0.0f;
+}
+
+template <bool kGuard = false>
+__device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o) {
+    double v[13];
+    observe_values<kGuard>(k, s, v);
+    write_obs_row(v, s.status, o);
+}
+
+// calc_reward(state, prev_state)['total'] of Actor_Critic_PPO.ipynb:164-263
+// (scalers: rl_helpers/scalers.py) on the frame's double observation `v`;
+// prev_dist is prev_state.distance_to_platform, NaN for prev_state None.  The
+// terms are summed in the notebook's order.  Branch-free (see frame()).
+__device__ __forceinline__ double notebook_reward(const double v[13], uint32_t status, double prev_dist) {
+    const double vx = v[2], vy = v[3], angle = v[4], fuel = v[6], dist = v[9], dx = v[10], dy = v[11],
+                 speed = v[12];
+    const bool have_prev = !__builtin_isnan(prev_dist);
+    const double delta = prev_dist - dist;
+    const double vtp = dist > 1e-6 ? (vx * dx + vy * dy) / dist : 0.0;  // velocity toward platform
+    const bool fast_toward = (speed >= 0.15) & (vtp > 0.1) & (dist > 0.065);
+    const double clipped = fmin(fmax(delta * 1000 * (1.0 + speed * 2.0), -2.0), 5.0);  // np.clip
+    const bool away = !fast_toward & (delta < -0.001);
+    double distance = fast_toward ? clipped : away ? -2.0 * fabs(delta) * 1000 : 0.0;
+    double hovering = (fast_toward | away) ? 0.0 : speed < 0.05 ? -1.0 : speed < 0.15 ? -0.3 : 0.0;
+    distance = have_prev ? distance : 0.0;
+    hovering = have_prev ? hovering : 0.0;
+    double total = 0.0;
+    total += -0.5;
+    total += distance;
+    total += hovering;
+    const double excess = fabs(angle) - (((0.20 - 0.111) * dist) + 0.111);
+    total += -(excess > 0.0 ? excess : 0.0);
+    const double over = dist < 1 ? speed - 0.1 : speed - 0.6;
+    total += (dist < 1 ? -2.0 : -1.0) * (over > 0.0 ? over : 0.0);
+    total += dy > 0.0 ? 0.0 : dy * 4.0;
+    const bool landed = status & DD_ST_LANDED, crashed = status & DD_ST_CRASHED;
+    const double crash_term = dist > 0.3 ? -200.0 - 100.0 : -200.0;
+    total += landed ? 800.0 + fuel * 100.0 : crashed ? crash_term : 0.0;
+    return total;
+}
+
+// element i of a lane array (i < kChunk)
+template <typename E>
+__device__ __forceinline__ E& at(E* base, uint32_t i) {
+    using B = typename std::conditional<std::is_const<E>::value, const char, char>::type;
+    return *reinterpret_cast<E*>(reinterpret_cast<B*>(base) + (uint32_t)(i * (uint32_t)sizeof(E)));
+}
+
+// A wave-uniform pointer the compiler cannot prove uniform (it comes from
+// threadIdx-derived arithmetic, or is hoisted into a VGPR), moved to SGPRs so
+// loads and stores use the SGPR-base + 32-bit lane offset form and its
+// arithmetic stays on the scalar unit.
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* q) {
+    const uint64_t v = reinterpret_cast<uint64_t>(q);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<P*>(((uint64_t)hi << 32) | lo);
+}
+
+// The state between two frames is what dd_step would store: rounded to the
+// storage width T (a no-op for double).
+// Under kRef the pad is static: px / py only change on a re-spawn, to
+// integers, which every storage width holds exactly.
+template <typename T, bool kRef = false>
+__device__ __forceinline__ void quantize(Lane& s) {
+    s.x = (T)s.x; s.y = (T)s.y; s.vx = (T)s.vx; s.vy = (T)s.vy; s.angle = (T)s.angle;
+    s.omega = (T)s.omega; s.fuel = (T)s.fuel; s.total = (T)s.total;
+    if constexpr (!kRef) { s.px = (T)s.px; s.py = (T)s.py; }
+}
+
+// The SoA of one batch (DDState) with typed pointers, offset to lane `first`.
+template <typename T>
+struct Soa {
+    T *x, *y, *vx, *vy, *angle, *omega, *fuel, *px, *py, *total;
+    uint8_t* status;
+    int32_t *steps, *episode;
+    int64_t env_id_base;
+};
+
+template <typename T>
+Soa<T> soa_of(const DDState& st, int64_t first) {
+    Soa<T> s;
+    s.x = (T*)st.x + first; s.y = (T*)st.y + first; s.vx = (T*)st.vx + first; s.vy = (T*)st.vy + first;
+    s.angle = (T*)st.angle + first; s.omega = (T*)st.omega + first; s.fuel = (T*)st.fuel + first;
+    s.px = (T*)st.px + first; s.py = (T*)st.py + first; s.total = (T*)st.total_reward + first;
+    s.status = st.status + first; s.steps = st.steps + first; s.episode = st.episode + first;
+    s.env_id_base = st.env_id_base + first;
+    return s;
+}
+
+inline bool state_ok(const DDState* st) {
+    return st && st->x && st->y && st->vx && st->vy && st->angle && st->omega && st->fuel && st->px &&
+           st->py && st->total_reward && st->status && st->steps && st->episode &&
+           (st->precision == DD_F32 || st->precision == DD_F64);
+}
+}  // namespace dd

@@ -41,82 +41,11 @@
 #include <stdint.h>
 
 #include "dronestep.h"
+#include "mlp_core.h"
 #include "philox.h"
 
 namespace dd {
 namespace mlp {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-constexpr int kIn = DD_OBS_DIM;  // 15
-#ifndef DD_MLP_WAVES
-#define DD_MLP_WAVES 8  // per block (one block per CU); experiments try 4 / 12
-#endif
-constexpr int kWaves = DD_MLP_WAVES;
-constexpr int kThreads = kWaves * 64;
-constexpr int kCols = 32;  // drones per wave tile
-
-// k-steps of 2 per layer (K = 16 for the 15 inputs + one zero column).
-constexpr int kSteps1 = 8, kSteps2 = 64, kSteps3 = 64;
-// Packed buffer (floats).  A sections are [out tile][k-step group of 4][lane][4]
-// (DD_MLP_F32) or, in the same space, [out tile][k-step of 16][hi | lo'][lane][8
-// halves] (DD_MLP_F16X3, pack_a16); the vector sections are shared.
-constexpr int kA1 = 0;
-constexpr int kA2 = kA1 + 4 * kSteps1 * 64;
-constexpr int kA3 = kA2 + 4 * kSteps2 * 64;
-constexpr int kV1 = kA3 + 2 * kSteps3 * 64;  // bias, LN weight, LN bias [3][128]
-constexpr int kV2 = kV1 + 3 * 128;
-constexpr int kV3 = kV2 + 3 * 128;  // [3][64]
-constexpr int kW4 = kV3 + 3 * 64;   // last layer [3][64], rows >= K zero
-constexpr int kB4 = kW4 + 3 * 64;   // bias [3], LayerNorm eps
-constexpr int kPacked = kB4 + 4;
-constexpr size_t kLdsBytes = kPacked * sizeof(float);
-static_assert(kPacked % 4 == 0, "packed buffer is read as float4");
-
-// Hidden row held in register r of accumulator tile t by lane half h
-// (C/D map of the 32x32 MFMAs on gfx950: row = (r&3) + 8(r>>2) + 4h).
-__host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h; }
-
-// ---- DD_MLP_F16X3: split operands on the f16 MFMA --------------------------
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr float kLoScale = 2048.0f;  // 2^11: lo' lives at hi's magnitude (no f16 subnormals)
-constexpr float kLoUnscale = 1.0f / 2048.0f;
-
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-
-// Two floats -> packed f16 hi and lo' halves, each rounded to nearest-even
-// (v_cvt_pk_f16_f32).  a - hi is exact in f32 (hi is a to 11 bits), the
-// scaling by 2^11 too.  (Truncating instead, v_cvt_pkrtz, biases lo' and
-// quadruples the end-to-end error: tools/mlp_split_sim.py --truncate.)
-// Written on float pairs so it lowers to v_cvt_pk_f16_f32, two
-// v_cvt_f32_f16, v_pk_add_f32, v_pk_mul_f32, v_cvt_pk_f16_f32 (6 VALU per
-// pair; scalar code had the compiler convert each half twice: 10).
-__device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
-    uint32_t hp = __builtin_bit_cast(uint32_t, f16x2{(_Float16)a, (_Float16)b});
-    asm("" : "+v"(hp));  // widen hi from the packed register (else each half is converted twice)
-    const f16x2 h = __builtin_bit_cast(f16x2, hp);
-    const f32x2 r = (f32x2{a, b} - f32x2{(float)h.x, (float)h.y}) * f32x2{kLoScale, kLoScale};
-    const f16x2 l = {(_Float16)r.x, (_Float16)r.y};
-    hi = hp;
-    lo = __builtin_bit_cast(uint32_t, l);
-}
-
-// Eight consecutive activations (one B fragment of a k-step) -> hi, lo'.
-__device__ __forceinline__ void split8(const float* v, f16x8& hi, f16x8& lo) {
-    u32x4 h, l;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        uint32_t a, b;
-        split_pair(v[2 * m], v[2 * m + 1], a, b);
-        h[m] = a;
-        l[m] = b;
-    }
-    hi = __builtin_bit_cast(f16x8, h);
-    lo = __builtin_bit_cast(f16x8, l);
-}
 
 // W[row][col] of layer 1 (cols >= 15 are the zero padding) or layers 2, 3.
 __device__ __forceinline__ float weight_at(const DDMlpParams& p, int base, int row, int col) {
@@ -189,148 +118,6 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
     out[i] = v;
 }
 
-// out^T tiles (NT of 32 rows) = bias + W . in^T over STEPS k-steps; bval(q)
-// is the lane's B operand (its column's input at the k of step q); bias_h =
-// the layer's bias + 4h (this lane half's rows).
-template <int NT, int STEPS, typename BVal>
-__device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lane, BVal bval, f32x16 (&acc)[NT],
-                                           const float* bias_h) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)  // the bias is the accumulator's initial value
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = bias_h[hid(t, r, 0)];
-#pragma unroll
-    for (int g = 0; g < STEPS / 4; ++g) {
-        f32x4 a[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) a[t] = a4[(t * (STEPS / 4) + g) * 64 + lane];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float b = bval(4 * g + j);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][j], b, acc[t], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep each group's LDS reads next to its MFMAs
-    }
-}
-
-// out^T tiles (NT of 32 rows) = bias + W . in^T over KS k-steps of 16.  The
-// packed A fragments are [tile][k-step][hi | lo'][lane] x 16 B; bh / bl are
-// the lane's B fragments.  The cross terms go first into the zeroed
-// accumulator, which is then scaled by 2^-11 and given the bias, and the
-// hi.hi products accumulate on top: one accumulator per tile.
-template <int NT, int KS>
-__device__ __forceinline__ void layer16(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
-                                        const f16x8 (&bl)[KS], f32x16 (&acc)[NT], const float* bias_h) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const u32x4* blk = a16 + (t * KS + s) * 128;
-            const f16x8 ah = __builtin_bit_cast(f16x8, blk[lane]);
-            const f16x8 al = __builtin_bit_cast(f16x8, blk[64 + lane]);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc[t], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep each k-step's LDS reads next to its MFMAs
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const f16x8 ah = __builtin_bit_cast(f16x8, a16[(t * KS + s) * 128 + lane]);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[t], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// x + (the same register of the other lane half), i.e. x + __shfl_xor(x, 32),
-// as one v_permlane32_swap (gfx950) instead of an LDS permute.  Lanes < 32
-// get x_l + x_{l+32}, lanes >= 32 x_{l-32} + x_l: the same sum (IEEE
-// addition is commutative).
-__device__ __forceinline__ float add_other_half(float x) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// LayerNorm over the column's 32*NT rows (biased variance, as nn.LayerNorm),
-// then ReLU.  vec = [Linear bias | LN weight | LN bias] of 32*NT each.  Pairs
-// of registers hold adjacent rows, so the arithmetic runs as packed f32
-// (v_pk_add / v_pk_fma), in torch's form y = (x * rstd - rstd * mean) *
-// weight + bias.
-template <int NT, typename Emit>
-__device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
-                                               Emit emit) {
-    constexpr int kRows = 32 * NT;
-    const float* gamma = vec + kRows + 4 * h;
-    const float* beta = vec + 2 * kRows + 4 * h;
-    f32x2 s2 = {0.0f, 0.0f};
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) s2 += f32x2{acc[t][r], acc[t][r + 1]};
-    const float sum = add_other_half(s2.x + s2.y);
-    const float mean = sum / (float)kRows;
-    const f32x2 m2 = {mean, mean};
-    f32x2 q2 = {0.0f, 0.0f};
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-            const f32x2 d = f32x2{acc[t][r], acc[t][r + 1]} - m2;
-            q2 = __builtin_elementwise_fma(d, d, q2);
-        }
-    const float sq = add_other_half(q2.x + q2.y);
-    const float rstd = 1.0f / sqrtf(sq / (float)kRows + eps);
-    const f32x2 rs2 = {rstd, rstd}, nb2 = {-rstd * mean, -rstd * mean};
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        float y[16];
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-            const int row = hid(t, r, 0);  // rows row, row + 1 (r even)
-            const f32x2 g = *reinterpret_cast<const f32x2*>(gamma + row);
-            const f32x2 b = *reinterpret_cast<const f32x2*>(beta + row);
-            const f32x2 xn = __builtin_elementwise_fma(f32x2{acc[t][r], acc[t][r + 1]}, rs2, nb2);
-            const f32x2 v = __builtin_elementwise_fma(xn, g, b);
-            y[r] = fmaxf(v.x, 0.0f);  // ReLU
-            y[r + 1] = fmaxf(v.y, 0.0f);
-        }
-        emit(t, y);
-        __builtin_amdgcn_sched_barrier(0);  // one tile's parameters in registers at a time
-    }
-}
-
-template <int NT>
-__device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
-                                          float (&y)[NT][16]) {
-    norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) y[t][r] = v[r];
-    });
-}
-
-// norm_relu straight into the next layer's split B fragments: k-step s takes
-// registers 8(s&1)..+7 of tile s>>1 (hidden rows hid(s>>1, 8(s&1)+j, h)),
-// the k order pack_a16 assumes.  No f32 copy of the activations stays live.
-template <int NT>
-__device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
-                                                f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
-    norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
-        split8(&v[0], bh[2 * t], bl[2 * t]);
-        split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
-    });
-}
-
 struct FwdArgs {
     const float* obs;
     float* out;
@@ -342,15 +129,6 @@ struct FwdArgs {
     int64_t n;
 };
 
-// log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
-// as torch's Bernoulli does (probs_to_logits, clamp_probs): log p or
-// log1p(-p).  (torch evaluates it as -BCE-with-logits of the logit; the two
-// agree to float32 rounding.)
-__device__ __forceinline__ float bernoulli_logp(float p, bool on) {
-    const float pc = fminf(fmaxf(p, FLT_EPSILON), 1.0f - FLT_EPSILON);
-    return on ? logf(pc) : log1pf(-pc);
-}
-
 template <int K, bool kSplit>
 __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__ packed, FwdArgs p) {
     extern __shared__ f32x4 lds4[];
@@ -359,88 +137,33 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
     __syncthreads();
 
     const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
-    const float eps = lds[kB4 + 3];
     const int64_t tiles = (p.n + kCols - 1) / kCols;
     for (int64_t tile = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); tile < tiles;
          tile += (int64_t)gridDim.x * kWaves) {
         const int64_t d = tile * kCols + c;  // this lane's drone (column)
         const bool live = d < p.n;
-        f32x16 acc4[4];
-        f32x16 acc2[2];
-        float y3[2][16];
-        if constexpr (kSplit) {
-            float x[8];  // the one k-step of layer 1: obs[d][8h + j]
+        float x[8];  // layer 1's B operands: obs[d][8h + q] (kSplit) or obs[d][2q + h]
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = 8 * h + j;
-                x[j] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
-            }
-            const u32x4* a16 = reinterpret_cast<const u32x4*>(lds);
-            f16x8 b1h[1], b1l[1], bh[8], bl[8];
-            split8(x, b1h[0], b1l[0]);
-            layer16<4, 1>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
-            norm_relu_split<4>(acc4, lds + kV1, eps, h, bh, bl);
-            layer16<4, 8>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
-            norm_relu_split<4>(acc4, lds + kV2, eps, h, bh, bl);
-            layer16<2, 8>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
-            norm_relu<2>(acc2, lds + kV3, eps, h, y3);
-        } else {
-            float y1[4][16], y2[4][16];
-            float x[kSteps1];  // B operands of layer 1: obs[d][2q + h]
-#pragma unroll
-            for (int q = 0; q < kSteps1; ++q) {
-                const int k = 2 * q + h;
-                x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
-            }
-            layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
-            norm_relu<4>(acc4, lds + kV1, eps, h, y1);
-            layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4,
-                                   lds + kV2 + 4 * h);
-            norm_relu<4>(acc4, lds + kV2, eps, h, y2);
-            layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2,
-                                   lds + kV3 + 4 * h);
-            norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        for (int q = 0; q < 8; ++q) {
+            const int k = kSplit ? 8 * h + q : 2 * q + h;
+            x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
         }
-        __builtin_amdgcn_sched_barrier(0);
-
-        float z[K];  // Linear(64, K): 32 rows per lane half, then the other half's
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float* w = lds + kW4 + k * 64 + 4 * h;
-            f32x2 s2 = {0.0f, 0.0f};
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; r += 2)
-                    s2 = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(w + hid(t, r, 0)),
-                                                   f32x2{y3[t][r], y3[t][r + 1]}, s2);
-            z[k] = add_other_half(s2.x + s2.y) + lds[kB4 + k];
-        }
+        float z[K];
+        mlp_body<K, kSplit>(lds, lane, x, z);
         if (!live || h != 0) continue;
         if constexpr (K == 1) {
             if (p.out) p.out[d] = z[0];
         } else {
-            float prob[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) prob[k] = 1.0f / (1.0f + expf(-z[k]));  // Sigmoid
+            float prob[3];
+            actor_probs(z, prob);
             if (p.out) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) p.out[d * K + k] = prob[k];
             }
             if (p.actions || p.log_prob) {
-                const uint64_t env = (uint64_t)(p.env_id_base + d), st = (uint64_t)p.step;
-                uint32_t r[4];
-                philox4x32_10((uint32_t)env, (uint32_t)(env >> 32), (uint32_t)st, (uint32_t)(st >> 32) ^ 0x5A5A5A5Au,
-                              (uint32_t)p.seed, (uint32_t)(p.seed >> 32), r);
-                uint32_t bits = 0;
-                float lp = 0.0f;
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const float u = (float)(r[k] >> 8) * 0x1p-24f;  // uniform [0, 1), 24 bits
-                    const bool on = u < prob[k];
-                    bits |= on ? (1u << k) : 0u;
-                    lp += bernoulli_logp(prob[k], on);
-                }
+                uint32_t bits;
+                float lp;
+                actor_sample(prob, (uint64_t)(p.env_id_base + d), (uint64_t)p.step, p.seed, bits, lp);
                 if (p.actions) p.actions[d] = (uint8_t)bits;
                 if (p.log_prob) p.log_prob[d] = lp;
             }

@@ -16,11 +16,11 @@ __all__ = [
     "DD_F32", "DD_F64", "DD_ACT_BITMASK", "DD_ACT_F32X3", "DD_ACT_U8X3", "DD_ACT_PHILOX",
     "DD_ST_DONE", "DD_ST_LANDED", "DD_ST_CRASHED", "DD_ST_PLAT_LEFT", "DD_OBS_DIM",
     "DD_RENDER_HUD", "DD_RENDER_GAME_OVER", "DD_MLP_F32", "DD_MLP_F16X3",
-    "DDConfig", "DDState", "DDStepIO", "DDRolloutIO", "DDMlpParams", "DDMlpIO", "lib", "load", "library_path", "check",
+    "DDConfig", "DDState", "DDStepIO", "DDRolloutIO", "DDMlpParams", "DDMlpIO", "DDPolicyRolloutIO", "lib", "load", "library_path", "check",
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 6
+DD_ABI_VERSION = 7
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
@@ -107,6 +107,16 @@ class DDMlpIO(ctypes.Structure):
     ]
 
 
+class DDPolicyRolloutIO(ctypes.Structure):
+    _fields_ = [
+        ("obs0", ctypes.c_void_p), ("obs_final", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+        ("actions", ctypes.c_void_p), ("log_prob", ctypes.c_void_p),
+        ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p),
+        ("seed", ctypes.c_uint64), ("step", ctypes.c_int64), ("frames", _I), ("max_steps", _I),
+        ("shaped_hist", ctypes.c_void_p), ("engine_reward", ctypes.c_void_p), ("engine_done", ctypes.c_void_p),
+    ]
+
+
 #: every symbol include/dronestep.h declares, with its ctypes signature
 EXPORTS = {
     "dd_config_default": (None, [ctypes.POINTER(DDConfig)]),
@@ -131,6 +141,8 @@ EXPORTS = {
     "dd_mlp_pack": (ctypes.c_int, [ctypes.POINTER(DDMlpParams), _I, ctypes.c_void_p, ctypes.c_void_p]),
     "dd_mlp_forward": (ctypes.c_int, [ctypes.c_void_p, _I, _I, ctypes.POINTER(DDMlpIO), ctypes.c_int64,
                                       ctypes.c_void_p]),
+    "dd_policy_rollout": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p, _I,
+                                         ctypes.POINTER(DDPolicyRolloutIO), ctypes.c_int64, ctypes.c_void_p]),
     "dd_render": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, _I,
                                  ctypes.c_void_p]),

@@ -123,6 +123,44 @@ def test_argument_errors_return_invalid_value_without_gpu():
     assert lib.dd_error_string(EINVAL)
 
 
+def test_policy_rollout_argument_errors_without_gpu():
+    lib = abi.lib()
+    cfg = EnvConfig().to_abi()
+    EINVAL = 1
+    assert ctypes.sizeof(abi.DDPolicyRolloutIO) == 7 * 8 + 8 + 8 + 4 + 4 + 3 * 8  # the C struct's layout
+    io = abi.DDPolicyRolloutIO()
+    io.obs0 = io.reward = io.done = 8
+    io.frames = 4
+
+    def run(state=None, packed=8, compute=abi.DD_MLP_F16X3, n=4, c=cfg):
+        st = state if state is not None else _state()
+        return lib.dd_policy_rollout(ctypes.byref(c) if c is not None else None, ctypes.byref(st), packed, compute,
+                                     ctypes.byref(io), n, None)
+
+    assert run(c=None) == EINVAL
+    assert run(state=abi.DDState()) == EINVAL  # null SoA pointers
+    assert run(state=_state(precision=7)) == EINVAL
+    assert run(n=-1) == EINVAL
+    assert run(compute=5) == EINVAL
+    assert run(packed=None) == EINVAL
+    io.obs0 = None
+    assert run() == EINVAL  # frame 0's policy input is required
+    io.obs0 = 8
+    io.reward = None
+    assert run() == EINVAL
+    io.reward = 8
+    io.engine_reward = 8  # engine outputs: both or neither, and only in notebook mode
+    assert run() == EINVAL
+    io.engine_done = 8
+    assert run() == EINVAL
+    io.engine_reward = io.engine_done = None
+    io.frames = -1
+    assert run() == EINVAL
+    io.frames = 0  # nothing to do (and no final observation wanted)
+    assert run() == 0
+    assert run(n=0) == 0
+
+
 def test_render_argument_errors_without_gpu():
     lib = abi.lib()
     cfg = EnvConfig().to_abi()

@@ -1,0 +1,137 @@
+"""GPU: dd_policy_rollout (collect_episodes_ppo with the actor in the loop,
+one launch) equals the two-kernel loop `actor.act(env.obs); env.step(a)`,
+bit for bit: policy inputs, samples, log-probabilities, rewards, dones, the
+final observation and state."""
+import pytest
+import torch
+from torch import nn
+
+import golden_data as gd
+from delivery_drone_amd import EnvConfig, MlpNet, VecDroneEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def actor(dev, seed, compute):
+    torch.manual_seed(seed)
+    net = nn.Sequential(nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128), nn.LayerNorm(128),
+                        nn.ReLU(), nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(), nn.Linear(64, 3))
+    with torch.no_grad():  # a policy that fires the main engine less often: longer, more varied episodes
+        net[9].bias.copy_(torch.tensor([-1.0, 0.0, 0.0]))
+    return MlpNet(net.state_dict(), device=dev, compute=compute)
+
+
+def twins(n, dev, precision="f32", reward_mode="engine", max_steps=300, env_id_base=0, **cfg):
+    c = EnvConfig(**cfg)
+    kw = dict(device=dev, config=c, precision=precision, reward_mode=reward_mode, max_steps=max_steps,
+              env_id_base=env_id_base)
+    a, b = VecDroneEnv(n, **kw), VecDroneEnv(n, **kw)
+    a.reset()
+    b.reset()
+    return a, b
+
+
+def assert_same_state(a, b):
+    for f in gd.FLOAT_FIELDS + ("status", "steps", "episode"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def loop(env, net, frames, seed, step):
+    """The reference shape of the collection loop, on the two kernels."""
+    obs, acts, lps, rews, dones, e_rews, e_dones = [], [], [], [], [], [], []
+    for k in range(frames):
+        obs.append(env.obs.clone())
+        a, lp = net.act(env.obs, seed=seed, step=step + k, env_id_base=env.env_id_base)
+        acts.append(a.clone())
+        lps.append(lp.clone())
+        _, r, d, info = env.step(a)
+        rews.append(r.clone())
+        dones.append(d.clone())
+        if env.reward_mode == "notebook":
+            e_rews.append(info["engine_reward"].clone())
+            e_dones.append(info["engine_done"].clone())
+    st = lambda xs: torch.stack(xs) if xs else None  # noqa: E731
+    return st(obs), st(acts), st(lps), st(rews), st(dones), st(e_rews), st(e_dones)
+
+
+@pytest.mark.parametrize("compute", ["f32", "f16x3"])
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("n", [1037, 2048])
+def test_policy_rollout_equals_act_step_loop(compute, precision, n, gpu_device):
+    frames, seed, step = 140, 11, 5
+    net = actor(gpu_device, 0, compute)
+    fused, ref = twins(n, gpu_device, precision, randomize_drone=True, auto_reset=True, seed=4)
+    obs, acts, lp, rew, done = fused.policy_rollout(net, frames, seed=seed, step=step)
+    r_obs, r_acts, r_lp, r_rew, r_done, _, _ = loop(ref, net, frames, seed, step)
+    assert torch.equal(obs, r_obs)
+    assert torch.equal(acts, r_acts)
+    assert torch.equal(lp, r_lp)
+    assert torch.equal(rew, r_rew)
+    assert torch.equal(done, r_done)
+    assert torch.equal(fused.obs, ref.obs)  # the bootstrap observation
+    assert_same_state(fused, ref)
+    assert int(fused.episode.max()) > 1 and bool(done.any())  # episodes ended and re-spawned inside the launch
+    assert 0 < int((acts & 1).sum()) < acts.numel()  # the policy's samples vary
+
+
+def test_policy_rollout_sticky_done_and_sharded_ids(gpu_device):
+    # auto_reset off: done lanes stay done (reward 0); a nonzero env id base keys the draws
+    n, frames = 300, 160
+    net = actor(gpu_device, 1, "f16x3")
+    fused, ref = twins(n, gpu_device, randomize_drone=True, seed=7, env_id_base=4096)
+    obs, acts, lp, rew, done = fused.policy_rollout(net, frames, seed=3)
+    r_obs, r_acts, r_lp, r_rew, r_done, _, _ = loop(ref, net, frames, 3, 0)
+    for got, want in zip((obs, acts, lp, rew, done), (r_obs, r_acts, r_lp, r_rew, r_done)):
+        assert torch.equal(got, want)
+    assert_same_state(fused, ref)
+    assert bool(done[-1].any())
+    assert torch.all(rew[-1][done[-2]] == 0)  # sticky done: reward 0 after the terminal frame
+
+
+@pytest.mark.parametrize("compute", ["f32", "f16x3"])
+def test_policy_rollout_notebook_reward_and_timeout(compute, gpu_device):
+    n, frames = 777, 90
+    net = actor(gpu_device, 2, compute)
+    fused, ref = twins(n, gpu_device, reward_mode="notebook", max_steps=40, randomize_drone=True, auto_reset=True,
+                       seed=5)
+    e_rew = torch.empty(frames, n, device=gpu_device)
+    e_done = torch.empty(frames, n, dtype=torch.bool, device=gpu_device)
+    obs, acts, lp, rew, done = fused.policy_rollout(net, frames, seed=1, engine_reward_out=e_rew,
+                                                    engine_done_out=e_done)
+    r_obs, r_acts, r_lp, r_rew, r_done, r_erew, r_edone = loop(ref, net, frames, 1, 0)
+    for got, want in zip((obs, acts, lp, rew, done, e_rew, e_done),
+                         (r_obs, r_acts, r_lp, r_rew, r_done, r_erew, r_edone)):
+        assert torch.equal(got, want)
+    assert torch.equal(fused.shaped_hist, ref.shaped_hist)
+    assert_same_state(fused, ref)
+    assert bool((ref.steps >= 0).all()) and bool(done.any())
+    assert bool((rew < -400).any())  # max_steps timeouts (-500) happened inside the launch
+
+
+def test_policy_rollout_many_blocks_and_options(gpu_device):
+    # 70,001 drones: more 8-wave blocks than CUs, a ragged last tile, rows not 16-byte aligned
+    n, frames = 70_001, 6
+    net = actor(gpu_device, 3, "f16x3")
+    fused, ref = twins(n, gpu_device, randomize_drone=True, auto_reset=True, seed=6)
+    obs, acts, lp, rew, done = fused.policy_rollout(net, frames, seed=2, step=100)
+    r_obs, r_acts, r_lp, r_rew, r_done, _, _ = loop(ref, net, frames, 2, 100)
+    for got, want in zip((obs, acts, lp, rew, done), (r_obs, r_acts, r_lp, r_rew, r_done)):
+        assert torch.equal(got, want)
+    assert torch.equal(fused.obs, ref.obs)
+    assert_same_state(fused, ref)
+    # record_obs=False and caller buffers; frames=0 changes nothing
+    before = {f: getattr(fused, f).clone() for f in gd.FLOAT_FIELDS}
+    o0 = fused.obs.clone()
+    out = fused.policy_rollout(net, 0, seed=2)
+    assert out[0].shape == (0, n, 15) and torch.equal(fused.obs, o0)
+    assert all(torch.equal(getattr(fused, f), v) for f, v in before.items())
+    acts_buf = torch.empty(2, n, dtype=torch.uint8, device=gpu_device)
+    obs2, acts2, _, _, _ = fused.policy_rollout(net, 2, seed=2, step=106, record_obs=False, actions_out=acts_buf)
+    loop(ref, net, 2, 2, 106)
+    assert obs2 is None and acts2.data_ptr() == acts_buf.data_ptr()
+    assert_same_state(fused, ref)
+    with pytest.raises(ValueError):
+        fused.policy_rollout(MlpNet(nn.Sequential(nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(),
+                                                  nn.Linear(128, 128), nn.LayerNorm(128), nn.ReLU(),
+                                                  nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(),
+                                                  nn.Linear(64, 1)).state_dict(), device=gpu_device), 2)

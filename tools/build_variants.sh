@@ -6,16 +6,17 @@ cd "$(dirname "$0")/../reinforcement-learning-101_amd"
 OUT=delivery_drone_amd/_native/lab
 mkdir -p $OUT
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I../include"
-build() { /opt/rocm/bin/hipcc $FLAGS "${@:2}" -o $OUT/lib_$1.so csrc/drone_step.hip csrc/policy_mlp.hip csrc/render.hip & }
+build() { /opt/rocm/bin/hipcc $FLAGS "${@:2}" -o $OUT/lib_$1.so csrc/drone_step.hip csrc/policy_mlp.hip csrc/policy_rollout.hip csrc/render.hip & }
 # "prev": the committed source at $PREV_REV (default HEAD), for before/after runs
 if [ -n "${PREV_REV:-HEAD}" ] && git -C .. rev-parse -q --verify "${PREV_REV:-HEAD}" > /dev/null 2>&1; then
   mkdir -p /tmp/dd_prev
   git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/drone_step.hip" > /tmp/dd_prev/drone_step.hip
   PREV_SRCS=/tmp/dd_prev/drone_step.hip
-  for f in trig.h philox.h policy_mlp.hip render.hip font_atlas.h; do
+  for f in trig.h philox.h frame.h mlp_core.h policy_mlp.hip policy_rollout.hip render.hip font_atlas.h; do
     git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/$f" > /tmp/dd_prev/$f 2>/dev/null || rm -f /tmp/dd_prev/$f
   done
   [ -f /tmp/dd_prev/policy_mlp.hip ] && PREV_SRCS="$PREV_SRCS /tmp/dd_prev/policy_mlp.hip"
+  [ -f /tmp/dd_prev/policy_rollout.hip ] && PREV_SRCS="$PREV_SRCS /tmp/dd_prev/policy_rollout.hip"
   [ -f /tmp/dd_prev/render.hip ] && PREV_SRCS="$PREV_SRCS /tmp/dd_prev/render.hip"
   /opt/rocm/bin/hipcc $FLAGS -Icsrc -o $OUT/lib_prev.so $PREV_SRCS &
 fi
