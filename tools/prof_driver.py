@@ -49,6 +49,18 @@ def main():
         lp = torch.empty(n, device=dev)
         for k in range(args.reps):
             actor.act(o, step=k, actions_out=acts_out, log_prob_out=lp)
+    elif args.what == "prl":  # dd_policy_rollout: actor + sampling + frame, `frames` per launch
+        from torch import nn
+        from delivery_drone_amd import MlpNet
+        torch.manual_seed(0)
+        net = nn.Sequential(nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128),
+                            nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(),
+                            nn.Linear(64, 3))
+        kw2 = {"library": lib} if lib is not None else {}
+        actor = MlpNet(net.state_dict(), device=dev, compute=args.compute, **kw2)
+        frames = min(args.frames, 64)
+        for k in range(args.reps):
+            env.policy_rollout(actor, frames, step=k * frames)
     elif args.what == "step":
         rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
         for k in range(args.reps):
