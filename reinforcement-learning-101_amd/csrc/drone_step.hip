@@ -377,6 +377,14 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
                  "s"(a.px), "s"(a.py), "s"(a.total), "s"(a.status), "s"(a.steps), "s"(p.actions));
     Raw<T> r;
     if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r);
+#ifdef DD_EXP_PAD_VALU  // timing-only: DD_EXP_PAD_VALU extra f64 FMAs per wave (4 chains), the VALU-cost slope
+    {
+        double pz[4] = {(double)r.x, (double)r.y, (double)r.vx, (double)r.vy};
+#pragma unroll
+        for (int q = 0; q < DD_EXP_PAD_VALU; ++q) asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(pz[q & 3]));
+        asm volatile("" ::"v"(pz[0]), "v"(pz[1]), "v"(pz[2]), "v"(pz[3]));
+    }
+#endif
 #ifdef DD_EXP_TIMELINE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     DD_TL(1);

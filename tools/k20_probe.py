@@ -1,0 +1,71 @@
+#!/usr/bin/env python
+"""Where the host time of a K = 20 timed region goes (config 3, one hipGraph
+of 20 dd_step launches, first replay of that graph as in bench.py):
+launch call, device time, synchronize return; torch's CUDAGraph.replay()
+against hipGraphLaunch on its raw exec handle through ctypes.
+"""
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
+import torch  # noqa: E402
+
+from delivery_drone_amd import EnvConfig, VecDroneEnv  # noqa: E402
+
+_hip = ctypes.CDLL("libamdhip64.so")
+_hip.hipGraphLaunch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    n, K, W = 262_144, 20, 5
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=0)
+    res = {}
+    for variant in ("torch", "raw", "torch", "raw", "torch", "raw"):
+        env = VecDroneEnv(n, device=dev, config=cfg)
+        env.reset()
+        rows = torch.randint(0, 8, (64, n), device=dev, dtype=torch.uint8)
+        stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(stream):
+            for i in range(3):
+                env.step(rows[i])
+            torch.cuda.synchronize(dev)
+            graphs = {}
+            for k in (K, W):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=stream):
+                    for i in range(k):
+                        env.step(rows[i])
+                graphs[k] = g
+            graphs[W].replay()
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(stream)
+            if variant == "torch":
+                graphs[K].replay()
+            else:
+                _hip.hipGraphLaunch(ctypes.c_void_p(graphs[K].raw_cuda_graph_exec()), ctypes.c_void_p(stream.cuda_stream))
+            t1 = time.perf_counter()
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+        dev_us = e0.elapsed_time(e1) * 1e3
+        r = res.setdefault(variant, {"launch_us": [], "wall_us": [], "dev_us": []})
+        r["launch_us"].append((t1 - t0) * 1e6)
+        r["wall_us"].append((t2 - t0) * 1e6)
+        r["dev_us"].append(dev_us)
+        del env, graphs
+        torch.cuda.empty_cache()
+    for v, r in res.items():
+        print(json.dumps({"variant": v, **{k: round(statistics.median(x), 2) for k, x in r.items()},
+                          "all_wall": [round(x, 1) for x in r["wall_us"]]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
