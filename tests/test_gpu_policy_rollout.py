@@ -135,3 +135,22 @@ def test_policy_rollout_many_blocks_and_options(gpu_device):
                                                   nn.Linear(128, 128), nn.LayerNorm(128), nn.ReLU(),
                                                   nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(),
                                                   nn.Linear(64, 1)).state_dict(), device=gpu_device), 2)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("cfg", [dict(platform_moving=True, auto_reset=True),
+                                 dict(wind_enabled=True, wind_x=0.05, wind_y=-0.02, auto_reset=False),
+                                 dict(gravity=0.31, auto_reset=True)])
+def test_policy_rollout_switches(cfg, precision, gpu_device):
+    """The kernels without compile-time physics (moving platform, wind,
+    non-reference constants; f64 is where ROCm 7.2 once miscompiled the
+    frame's observation, tools/scan_isa.py): still the act+step loop."""
+    n, frames = 515, 70
+    net = actor(gpu_device, 4, "f16x3")
+    fused, ref = twins(n, gpu_device, precision, randomize_drone=True, seed=12, **cfg)
+    got = fused.policy_rollout(net, frames, seed=8)
+    want = loop(ref, net, frames, 8, 0)[:5]
+    for g, w in zip(got, want):
+        assert torch.equal(g, w)
+    assert torch.equal(fused.obs, ref.obs)
+    assert_same_state(fused, ref)
