@@ -480,9 +480,16 @@ def policy_fused_point(n, frames, seed, dev, compute="f16x3", reps=5):
     tfs = n * frames * MLP_FLOPS_PER_ROW / (ms * 1e-3) / 1e12
     del actor, env, bufs
     torch.cuda.empty_cache()
+    if compute == "f32":
+        roof = {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_drone_frame": MLP_FLOPS_PER_ROW}
+    else:  # three f16 MFMAs per product, as policy_point prices them
+        roof = {"bound": "mfma", "achieved": round(3 * tfs, 2), "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(3 * tfs / F16_MFMA_PEAK_TFS, 4), "flops_per_drone_frame": 3 * MLP_FLOPS_PER_ROW,
+                "algorithmic_tflops": round(tfs, 2)}
     return {"envs": n, "frames": frames, "compute": compute, "ms": round(ms, 3),
             "steps_per_s": round(n * frames / (ms * 1e-3), 1), "us_per_frame": round(ms * 1e3 / frames, 2),
-            "actor_tflops": round(tfs, 2), "launch": f"one dd_policy_rollout launch per {frames} frames",
+            "roofline": roof, "launch": f"one dd_policy_rollout launch per {frames} frames",
             "kernel": f"dd::prl::policy_rollout_kernel<float, {'true' if compute == 'f16x3' else 'false'}, true>"}
 
 
