@@ -52,6 +52,8 @@ class MlpNet:
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("MlpNet runs on the GPU (HIP); there is no CPU path")
+        if self.device.index is None:  # "cuda" -> the current device, as VecDroneEnv does
+            self.device = torch.device("cuda", torch.cuda.current_device())
         if compute not in _COMPUTE:
             raise ValueError(f"compute must be one of {sorted(_COMPUTE)}, got {compute!r}")
         self.compute = compute

@@ -154,3 +154,17 @@ def test_policy_rollout_switches(cfg, precision, gpu_device):
         assert torch.equal(g, w)
     assert torch.equal(fused.obs, ref.obs)
     assert_same_state(fused, ref)
+
+
+def test_policy_rollout_default_devices(gpu_device):
+    # MlpNet(device="cuda") and VecDroneEnv() with no device name the same GPU
+    torch.manual_seed(5)
+    net = nn.Sequential(nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128), nn.LayerNorm(128),
+                        nn.ReLU(), nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(), nn.Linear(64, 3))
+    with torch.cuda.device(gpu_device):
+        actor_ = MlpNet(net.state_dict())
+        env = VecDroneEnv(96, randomize_drone=True, auto_reset=True)
+        env.reset()
+        obs, acts, lp, rew, done = env.policy_rollout(actor_, 3)
+    assert actor_.device == env.device
+    assert obs.shape == (3, 96, 15) and acts.shape == (3, 96) and bool(torch.isfinite(lp).all())
