@@ -231,6 +231,17 @@ __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* 
 template <int NT>
 __device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                 f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
+#ifdef DD_MLP_PAD  // timing-only: DD_MLP_PAD extra packed f32 FMAs (8 chains) per split layer, the VALU-cost slope
+    {
+        f32x2 pz[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pz[q] = f32x2{acc[0][q], acc[0][q + 8]};
+#pragma unroll
+        for (int q = 0; q < DD_MLP_PAD; ++q) asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(pz[q & 7]));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) asm volatile("" ::"v"(pz[q]));
+    }
+#endif
     norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
         split8(&v[0], bh[2 * t], bl[2 * t]);
         split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);

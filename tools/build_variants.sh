@@ -56,6 +56,7 @@ for v in ${VARIANTS:-base}; do
     tlwtall) build tlwtall -DDD_EXP_TIMELINE -DDD_ST_STATE=1 -DDD_ST_OUT=1 -DDD_ST_OBS=1 ;;
     ieeerstd) build ieeerstd -DDD_MLP_IEEE_RSTD ;;
     pad*) build $v -DDD_EXP_PAD_VALU=${v#pad} ;;
+    mpad*) build $v -DDD_MLP_PAD=${v#mpad} ;;
     tl_s*_o*)  # timeline + store policies: tl_s<state>_o<out and obs>, values as DD_ST_* (>= 100: raw aux bits)
       s=${v#tl_s}; s=${s%%_o*}; o=${v##*_o}
       build $v -DDD_EXP_TIMELINE -DDD_ST_STATE=$s -DDD_ST_OUT=$o -DDD_ST_OBS=$o ;;
