@@ -1,0 +1,67 @@
+#!/usr/bin/env python
+"""A/B timing of dd_gae builds over [T, N] float32 buffers, interleaved
+rounds; prints us and TB/s (17 B per element) per variant and size."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
+import torch  # noqa: E402
+
+from delivery_drone_amd import abi  # noqa: E402
+
+LAB = os.path.join(REPO, "reinforcement-learning-101_amd", "delivery_drone_amd", "_native", "lab")
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--variants", default="base")
+    p.add_argument("--shapes", default="256x65536,256x262144,64x1048576")
+    p.add_argument("--rounds", type=int, default=12)
+    args = p.parse_args()
+    dev = torch.device("cuda", 0)
+    libs = {v: abi.load(os.path.join(LAB, f"lib_{v}.so")) for v in args.variants.split(",")}
+    for shape in args.shapes.split(","):
+        T, n = (int(x) for x in shape.split("x"))
+        r = torch.randn(T, n, device=dev)
+        v = torch.randn(T + 1, n, device=dev)
+        d = (torch.rand(T, n, device=dev) < 0.01).to(torch.uint8)
+        adv = torch.empty(T, n, device=dev)
+        ret = torch.empty(T, n, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        times = {k: [] for k in libs}
+        ref = None
+        for name, lib in libs.items():
+            lib.dd_gae(r.data_ptr(), v.data_ptr(), d.data_ptr(), adv.data_ptr(), ret.data_ptr(), T, n, 0.99, 0.95,
+                       ctypes.c_void_p(stream))
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = adv.clone()
+            elif not torch.equal(ref, adv):
+                print(json.dumps({"variant": name, "MISMATCH": True}), flush=True)
+        names = list(libs)
+        for rnd in range(args.rounds):
+            for name in (names if rnd % 2 == 0 else names[::-1]):
+                lib = libs[name]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    lib.dd_gae(r.data_ptr(), v.data_ptr(), d.data_ptr(), adv.data_ptr(), ret.data_ptr(), T, n, 0.99,
+                               0.95, ctypes.c_void_p(stream))
+                e1.record()
+                torch.cuda.synchronize()
+                times[name].append(e0.elapsed_time(e1) * 1e3 / 5)
+        for name, ts in times.items():
+            us = statistics.median(ts)
+            print(json.dumps({"T": T, "envs": n, "variant": name, "us_median": round(us, 2),
+                              "tbs": round((17 * T * n + 4 * n) / (us * 1e-6) / 1e12, 3)}), flush=True)
+        del r, v, d, adv, ret
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
