@@ -46,6 +46,16 @@ constexpr int kPacked = kB4 + 4;
 constexpr size_t kLdsBytes = kPacked * sizeof(float);
 static_assert(kPacked % 4 == 0, "packed buffer is read as float4");
 
+// The three hidden Linears are packed mean-centred over their outputs
+// (policy_mlp.hip weight_at), so the LayerNorm that follows each skips its
+// mean pass (-DDD_MLP_UNCENTERED: the plain weights and the two-pass
+// LayerNorm, for A/B).
+#ifdef DD_MLP_UNCENTERED
+constexpr bool kCentered = false;
+#else
+constexpr bool kCentered = true;
+#endif
+
 // Hidden row held in register r of accumulator tile t by lane half h
 // (C/D map of the 32x32 MFMAs on gfx950: row = (r&3) + 8(r>>2) + 4h).
 __host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h; }
@@ -173,20 +183,22 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
     constexpr int kRows = 32 * NT;
     const float* gamma = vec + kRows + 4 * h;
     const float* beta = vec + 2 * kRows + 4 * h;
-    f32x2 s2 = {0.0f, 0.0f};
+    float mean = 0.0f;  // centred weights: the column's mean is zero to rounding
+    if constexpr (!kCentered) {
+        f32x2 s2 = {0.0f, 0.0f};
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) s2 += f32x2{acc[t][r], acc[t][r + 1]};
-    const float sum = add_other_half(s2.x + s2.y);
-    const float mean = sum / (float)kRows;
+            for (int r = 0; r < 16; r += 2) s2 += f32x2{acc[t][r], acc[t][r + 1]};
+        mean = add_other_half(s2.x + s2.y) / (float)kRows;
+    }
     const f32x2 m2 = {mean, mean};
     f32x2 q2 = {0.0f, 0.0f};
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-            const f32x2 d = f32x2{acc[t][r], acc[t][r + 1]} - m2;
+            const f32x2 d = kCentered ? f32x2{acc[t][r], acc[t][r + 1]} : f32x2{acc[t][r], acc[t][r + 1]} - m2;
             q2 = __builtin_elementwise_fma(d, d, q2);
         }
     const float sq = add_other_half(q2.x + q2.y);

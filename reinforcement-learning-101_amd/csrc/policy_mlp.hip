@@ -47,10 +47,28 @@
 namespace dd {
 namespace mlp {
 
-// W[row][col] of layer 1 (cols >= 15 are the zero padding) or layers 2, 3.
+// W[row][col] of layer 1 (cols >= 15 are the zero padding) or layers 2, 3,
+// centred over its output rows (kCentered, mlp_core.h): W - 1 (1^T W) / rows,
+// in double, rounded once.  Every layer here feeds a LayerNorm, which only
+// sees its input minus the input's mean: with centred weights and bias the
+// GEMM's output already has (to rounding) zero mean, and norm_relu_emit skips
+// the mean pass.
 __device__ __forceinline__ float weight_at(const DDMlpParams& p, int base, int row, int col) {
-    if (base == kA1) return col < kIn ? p.w0[row * kIn + col] : 0.0f;
-    return (base == kA2 ? p.w3 : p.w6)[row * 128 + col];
+    if (base == kA1 && col >= kIn) return 0.0f;
+    const float* w = base == kA1 ? p.w0 : base == kA2 ? p.w3 : p.w6;
+    const int cols = base == kA1 ? kIn : 128, rows = base == kA3 ? 64 : 128;
+    if (!kCentered) return w[row * cols + col];
+    double sum = 0.0;
+    for (int r = 0; r < rows; ++r) sum += (double)w[r * cols + col];
+    return (float)((double)w[row * cols + col] - sum / rows);
+}
+
+// A Linear bias before a LayerNorm, centred like its weights.
+__device__ __forceinline__ float bias_at(const float* b, int rows, int o) {
+    if (!kCentered) return b[o];
+    double sum = 0.0;
+    for (int r = 0; r < rows; ++r) sum += (double)b[r];
+    return (float)((double)b[o] - sum / rows);
 }
 
 // DD_MLP_F16X3 A fragments, one packed float = two halves: section
@@ -89,25 +107,22 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
         const int j = o & 3, l = (o >> 2) & 63, grp = o >> 8;
         const int t = grp / (steps / 4), q = 4 * (grp % (steps / 4)) + j;
         const int row = 32 * t + (l & 31), h = l >> 5;
-        if (base == kA1) {  // layer 1: natural k order, column 15 is zero
-            const int col = 2 * q + h;
-            v = col < kIn ? p.w0[row * kIn + col] : 0.0f;
-        } else {  // layers 2, 3: k-step (t', r) = q takes hidden row hid(t', r, h)
-            const int col = hid(q >> 4, q & 15, h);
-            v = (base == kA2 ? p.w3 : p.w6)[row * 128 + col];
-        }
+        // layer 1: natural k order, column 15 is zero; layers 2, 3: k-step
+        // (t', r) = q takes hidden row hid(t', r, h)
+        const int col = base == kA1 ? 2 * q + h : hid(q >> 4, q & 15, h);
+        v = weight_at(p, base, row, col);
     } else if (i < kV2) {
         const int o = i - kV1;
         const float* src[3] = {p.b0, p.ln1_w, p.ln1_b};
-        v = src[o / 128][o % 128];
+        v = o < 128 ? bias_at(p.b0, 128, o) : src[o / 128][o % 128];
     } else if (i < kV3) {
         const int o = i - kV2;
         const float* src[3] = {p.b3, p.ln4_w, p.ln4_b};
-        v = src[o / 128][o % 128];
+        v = o < 128 ? bias_at(p.b3, 128, o) : src[o / 128][o % 128];
     } else if (i < kW4) {
         const int o = i - kV3;
         const float* src[3] = {p.b6, p.ln7_w, p.ln7_b};
-        v = src[o / 64][o % 64];
+        v = o < 64 ? bias_at(p.b6, 64, o) : src[o / 64][o % 64];
     } else if (i < kB4) {
         const int o = i - kW4;
         v = (o / 64) < p.out_dim ? p.w9[o] : 0.0f;

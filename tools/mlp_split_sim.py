@@ -3,12 +3,15 @@
 (tests/golden/policy.npz): max probability / value error against float64, next
 to plain float32.  Operands split as a = hi + lo * 2^-11 with hi, lo f16
 (both rounded to nearest-even: truncating them, v_cvt_pkrtz, biases lo and
-quadruples the error; run with --truncate), products exact, sums rounded to f32."""
+quadruples the error; run with --truncate), products exact, sums rounded to f32.
+--center: the hidden Linears mean-centred over their outputs and the LayerNorm
+without its mean pass, as dd_mlp_pack / norm_relu_emit do (mlp_core.h kCentered)."""
 import sys
 
 import numpy as np
 
 TRUNCATE = '--truncate' in sys.argv
+CENTER = '--center' in sys.argv
 d = np.load(__import__('os').path.join(__import__('os').path.dirname(__import__('os').path.abspath(__file__)), '..', 'tests', 'golden', 'policy.npz'))
 def rtz16(x):
     """float32 -> float16 rounded toward zero (v_cvt_pkrtz_f16_f32)."""
@@ -39,12 +42,19 @@ def lin(W, x, b, mode):
     return (main.astype(np.float32) + (cross.astype(np.float32) * np.float32(2**-11))).astype(np.float32) + b
 def ln(x, w, b, mode):
     dt = np.float64 if mode == 'f64' else np.float32
-    x = x.astype(dt); m = x.mean(1, keepdims=True); v = ((x - m) ** 2).mean(1, keepdims=True)
+    x = x.astype(dt); m = x.mean(1, keepdims=True)
+    if CENTER and mode != 'f64':
+        m = np.zeros_like(m)  # the centred GEMM's output: mean zero to rounding
+    v = ((x - m) ** 2).mean(1, keepdims=True)
     return np.maximum((x - m) / np.sqrt(v + 1e-5) * w + b, 0)
 def fwd(pre, mode):
     x = d['obs']
     for i, j in ((0, 1), (3, 4), (6, 7)):
-        x = lin(d[f'{pre}.network.{i}.weight'], x, d[f'{pre}.network.{i}.bias'], mode)
+        W, b = d[f'{pre}.network.{i}.weight'], d[f'{pre}.network.{i}.bias']
+        if CENTER and mode != 'f64':
+            W = (W.astype(np.float64) - W.astype(np.float64).mean(0, keepdims=True)).astype(np.float32)
+            b = (b.astype(np.float64) - b.astype(np.float64).mean()).astype(np.float32)
+        x = lin(W, x, b, mode)
         x = ln(x, d[f'{pre}.network.{j}.weight'], d[f'{pre}.network.{j}.bias'], mode)
     z = lin(d[f'{pre}.network.9.weight'], x, d[f'{pre}.network.9.bias'], 'f64' if mode == 'f64' else 'f32')
     return z
