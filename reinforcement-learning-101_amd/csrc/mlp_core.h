@@ -281,9 +281,15 @@ __device__ __forceinline__ float bernoulli_logp(float p, bool on) {
 // for the 32 drones of one wave tile: lane (c, h) holds column c's inputs
 // x[q] = obs[c][2q + h] (DD_MLP_F32, k-steps of 2) or obs[c][8h + q]
 // (kSplit, one k-step of 16), zero past column 14.  Every lane ends with z
-// of its column.  lds: the packed parameters.
-template <int K, bool kSplit>
-__device__ __forceinline__ void mlp_body(const float* lds, int lane, const float (&x)[8], float (&z)[K]) {
+// of its column.  lds: the packed parameters.  mid() runs between layer 1
+// and layer 2 (dd_mlp_forward waits there for layers 2-3 of its LDS image).
+struct NoMid {
+    __device__ void operator()() const {}
+};
+
+template <int K, bool kSplit, typename Mid = NoMid>
+__device__ __forceinline__ void mlp_body(const float* lds, int lane, const float (&x)[8], float (&z)[K],
+                                         Mid mid = {}) {
     const f32x4* lds4 = reinterpret_cast<const f32x4*>(lds);
     const int h = lane >> 5;
     const float eps = lds[kB4 + 3];
@@ -296,6 +302,7 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
         split8(x, b1h[0], b1l[0]);
         layer16<4, 1>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
         norm_relu_split<4>(acc4, lds + kV1, eps, h, bh, bl);
+        mid();
         layer16<4, 8>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
         norm_relu_split<4>(acc4, lds + kV2, eps, h, bh, bl);
         layer16<2, 8>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
@@ -304,6 +311,7 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
         float y1[4][16], y2[4][16];
         layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
         norm_relu<4>(acc4, lds + kV1, eps, h, y1);
+        mid();
         layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4,
                                lds + kV2 + 4 * h);
         norm_relu<4>(acc4, lds + kV2, eps, h, y2);

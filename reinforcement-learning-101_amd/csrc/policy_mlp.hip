@@ -144,27 +144,65 @@ struct FwdArgs {
     int64_t n;
 };
 
+// Layer 1's B operands for lane (c, h) of a tile: obs[d][8h + q] (kSplit) or
+// obs[d][2q + h], zero past column 14 and past the last row.
+template <bool kSplit>
+__device__ __forceinline__ void load_inputs(const FwdArgs& p, int64_t tile, int lane, float (&x)[8]) {
+    const int h = lane >> 5;
+    const int64_t d = tile * kCols + (lane & 31);
+    const bool live = d < p.n;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int k = kSplit ? 8 * h + q : 2 * q + h;
+        x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
+    }
+}
+
+// The LDS image arrives in two parts.  Layer 1's fragments and the vector
+// sections (13 KB) are register-staged before the block's first barrier;
+// layers 2-3 (96 KB, [kA2, kV1)) go by LDS-DMA (global_load_lds_dwordx4, 1 KB
+// per wave-instruction, the LDS image lane-linear like the packed buffer) and
+// stay in flight while every wave runs layer 1 of its first tile; the second
+// barrier, after a vmcnt(0), comes between layer 1 and layer 2 of that tile.
+// Raw s_barrier, not __syncthreads() (whose fence would drain the DMA at the
+// first barrier), and the first tile's observation is waited for before the
+// DMA is issued (hipcc waits vmcnt(0) at the first use of any ordinary load
+// made while a DMA is outstanding).
 template <int K, bool kSplit>
 __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__ packed, FwdArgs p) {
     extern __shared__ f32x4 lds4[];
     const float* lds = reinterpret_cast<const float*>(lds4);
-    for (int i = threadIdx.x; i < kPacked / 4; i += kThreads) lds4[i] = reinterpret_cast<const f32x4*>(packed)[i];
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
     const int64_t tiles = (p.n + kCols - 1) / kCols;
-    for (int64_t tile = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); tile < tiles;
-         tile += (int64_t)gridDim.x * kWaves) {
+    int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
+    float x[8];
+    load_inputs<kSplit>(p, tile, lane, x);
+    const f32x4* src4 = reinterpret_cast<const f32x4*>(packed);
+    for (int i = threadIdx.x; i < kA2 / 4; i += kThreads) lds4[i] = src4[i];
+    for (int i = kV1 / 4 + threadIdx.x; i < kPacked / 4; i += kThreads) lds4[i] = src4[i];
+    asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+    constexpr int kChunk = 64 * 4;  // floats per wave-instruction
+    static_assert((kV1 - kA2) % kChunk == 0 && kA2 % kChunk == 0, "DMA chunks");
+    for (int q = wave; q < (kV1 - kA2) / kChunk; q += kWaves) {
+        const int off = kA2 + q * kChunk;
+        __builtin_amdgcn_global_load_lds(packed + off + lane * 4, lds4 + off / 4, 16, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    bool first = true;
+    const auto mid = [&first] {
+        if (first) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            first = false;
+        }
+    };
+    for (; tile < tiles; tile += (int64_t)gridDim.x * kWaves) {
+        if (!first) load_inputs<kSplit>(p, tile, lane, x);
         const int64_t d = tile * kCols + c;  // this lane's drone (column)
         const bool live = d < p.n;
-        float x[8];  // layer 1's B operands: obs[d][8h + q] (kSplit) or obs[d][2q + h]
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int k = kSplit ? 8 * h + q : 2 * q + h;
-            x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
-        }
         float z[K];
-        mlp_body<K, kSplit>(lds, lane, x, z);
+        mlp_body<K, kSplit>(lds, lane, x, z, mid);
         if (!live || h != 0) continue;
         if constexpr (K == 1) {
             if (p.out) p.out[d] = z[0];
@@ -184,6 +222,7 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
             }
         }
     }
+    mid();  // a wave without a tile still takes its part in the second barrier
 }
 
 template <int K, bool kSplit>
