@@ -139,7 +139,7 @@ static float time_graph(hipStream_t st, int launches, F launch) {
     return sum / reps * 1e3f / launches;
 }
 
-int main() {
+int main(int argc, char** argv) {
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     const int G = 1024;
@@ -157,7 +157,8 @@ int main() {
                time_graph(st, 100, [&] { hipLaunchKernelGGL(empty_lds_karg, dim3(G), dim3(256), 0, st, G, b, sink); }));
         fflush(stdout);
     }
-    const uint32_t n = 262144;
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 262144u;  // drones (the copy cases)
+    const int G2 = (int)(n / 256);
     Arrs a;
     for (int r = 0; r < 12; ++r) {
         float* p;
@@ -170,11 +171,17 @@ int main() {
     CK(hipMalloc(&a.done, n));
     for (int rep = 0; rep < 2; ++rep) {
         printf("{\"case\": \"copy_strided_obs\", \"us\": %.3f}\n",
-               time_graph(st, 100, [&] { hipLaunchKernelGGL((copy_kernel<false>), dim3(G), dim3(256), 0, st, a, n); }));
+               time_graph(st, 100, [&] { hipLaunchKernelGGL((copy_kernel<false>), dim3(G2), dim3(256), 0, st, a, n); }));
         printf("{\"case\": \"copy_lds_obs\", \"us\": %.3f}\n",
-               time_graph(st, 100, [&] { hipLaunchKernelGGL((copy_kernel<true>), dim3(G), dim3(256), 0, st, a, n); }));
+               time_graph(st, 100, [&] { hipLaunchKernelGGL((copy_kernel<true>), dim3(G2), dim3(256), 0, st, a, n); }));
         auto stamped = [&](const char* name, auto kern) {
-            const float us = time_graph(st, 100, [&] { hipLaunchKernelGGL(kern, dim3(G), dim3(256), 0, st, a, n); });
+            if (n != 262144u) {  // the stamp buffer covers config 3's 4,096 waves
+                printf("{\"case\": \"%s\", \"n\": %u, \"us\": %.3f}\n", name, n,
+                       time_graph(st, 20, [&] { hipLaunchKernelGGL(kern, dim3(G2), dim3(256), 0, st, a, n); }));
+                fflush(stdout);
+                return;
+            }
+            const float us = time_graph(st, 100, [&] { hipLaunchKernelGGL(kern, dim3(G2), dim3(256), 0, st, a, n); });
             uint64_t tl[4096 * 2];
             CK(hipMemcpyFromSymbol(tl, HIP_SYMBOL(tl_buf), sizeof(tl), 0, hipMemcpyDeviceToHost));
             uint64_t lo = ~0ull, hi = 0;
@@ -198,7 +205,7 @@ int main() {
         stamped("inplace_stepmix_stamped", copy_kernel<true, true, 2>);
         std::swap(a, ip);
         printf("{\"case\": \"copy_lds_obs_stepmix\", \"us\": %.3f}\n",
-               time_graph(st, 100, [&] { hipLaunchKernelGGL((copy_kernel<true, false, 2>), dim3(G), dim3(256), 0, st, a, n); }));
+               time_graph(st, 100, [&] { hipLaunchKernelGGL((copy_kernel<true, false, 2>), dim3(G2), dim3(256), 0, st, a, n); }));
         fflush(stdout);
     }
     return 0;
