@@ -60,9 +60,10 @@ enum {
     DD_ACT_F32X3 = 1,   /* float[N][3] (main, left, right), nonzero = on;     */
                         /* the notebooks' Bernoulli(probs).sample() layout     */
     DD_ACT_U8X3 = 2,    /* uint8/bool[N][3] (main, left, right), nonzero = on */
-    DD_ACT_PHILOX = 3   /* dd_rollout only: no action buffer; each frame's
-                           bitmask is Philox4x32-10(key = action_seed,
-                           ctr = {env, step}) & 7 — a uniform random policy */
+    DD_ACT_PHILOX = 3   /* dd_rollout only: no action buffer; step s's
+                           bitmask is byte s & 15 of Philox4x32-10(key =
+                           action_seed, ctr = {env, s >> 4}) & 7 — a uniform
+                           random policy, one block per 16 steps            */
 };
 
 /* Status byte bits (DDState.status). */

@@ -83,14 +83,18 @@ def test_rollout_without_obs_and_zero_frames(gpu_device):
 
 
 def philox_actions(seed, env0, n, step0, k):
+    """include/dronestep.h DD_ACT_PHILOX: step s's bitmask is byte s & 15 of
+    the Philox4x32-10 block (key seed; ctr env, s >> 4), low 3 bits."""
     key = [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF]
     out = np.zeros((k, n), dtype=np.uint8)
     for t in range(k):
         s = step0 + t
+        b = s >> 4
         for i in range(n):
             e = env0 + i
-            ctr = [e & 0xFFFFFFFF, e >> 32, s & 0xFFFFFFFF, (s >> 32) ^ 0xA5A5A5A5]
-            out[t, i] = ora.philox4x32_10(ctr, key)[0] & 7
+            ctr = [e & 0xFFFFFFFF, e >> 32, b & 0xFFFFFFFF, (b >> 32) ^ 0xA5A5A5A5]
+            word = ora.philox4x32_10(ctr, key)[(s >> 2) & 3]
+            out[t, i] = (word >> (8 * (s & 3))) & 7
     return out
 
 
@@ -107,6 +111,27 @@ def test_rollout_philox_policy(gpu_device):
         o, r, d, _ = loop.step(acts[t])
         assert torch.equal(obs[t], o) and torch.equal(reward[t], r), t
     assert_same_state(roll, loop)
+    assert len({int(a) for a in acts.flatten()}) == 8  # every bitmask drawn
+
+
+def test_rollout_philox_actions_do_not_depend_on_launch_split(gpu_device):
+    # 37 frames from step 5 (blocks of 16 steps: 0-15, 16-31, 32-47) as one launch
+    # and as launches of 9, 1, 14, 13 frames: the same actions, the same rollout
+    n, k = 200, 37
+    c = EnvConfig(randomize_drone=True, auto_reset=True, seed=9)
+    one = VecDroneEnv(n, device=gpu_device, config=c)
+    split = VecDroneEnv(n, device=gpu_device, config=c)
+    one.reset()
+    split.reset()
+    obs, reward, done = one.rollout(frames=k, action_seed=3, action_step=5)
+    parts, t0 = [], 0
+    for m in (9, 1, 14, 13):
+        parts.append(split.rollout(frames=m, action_seed=3, action_step=5 + t0))
+        t0 += m
+    assert torch.equal(obs, torch.cat([q[0] for q in parts]))
+    assert torch.equal(reward, torch.cat([q[1] for q in parts]))
+    assert torch.equal(done, torch.cat([q[2] for q in parts]))
+    assert_same_state(one, split)
 
 
 def test_rollout_philox_sharding_invariant(gpu_device):

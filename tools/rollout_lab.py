@@ -21,6 +21,7 @@ def main():
     p.add_argument("--frames", type=int, default=256)
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--no-obs", action="store_true")
+    p.add_argument("--philox", action="store_true", help="in-kernel Philox actions (config 5b) instead of a tensor")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     cfg = EnvConfig(randomize_drone=True, auto_reset=True, seed=0)
@@ -33,7 +34,8 @@ def main():
         for v in args.variants.split(","):
             e = VecDroneEnv(n, device=dev, config=cfg, library=abi.load(os.path.join(LAB, f"lib_{v}.so")))
             e.reset()
-            e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done, write_obs=not args.no_obs)
+            e.rollout(None if args.philox else acts, frames=args.frames, obs_out=obs, reward_out=rew, done_out=done,
+                      write_obs=not args.no_obs)
             envs[v] = (e, [])
         torch.cuda.synchronize()
         names = list(envs)
@@ -42,13 +44,14 @@ def main():
                 e, ts = envs[v]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                e.rollout(acts, obs_out=obs, reward_out=rew, done_out=done, write_obs=not args.no_obs)
+                e.rollout(None if args.philox else acts, frames=args.frames, obs_out=obs, reward_out=rew,
+                          done_out=done, write_obs=not args.no_obs)
                 e1.record()
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1))
         for v, (e, ts) in envs.items():
             med = statistics.median(ts)
-            print(json.dumps({"envs": n, "frames": args.frames, "variant": v, "obs": not args.no_obs,
+            print(json.dumps({"envs": n, "frames": args.frames, "variant": v, "obs": not args.no_obs, "philox": args.philox,
                               "ms_median": round(med, 4),
                               "steps_per_s": round(n * args.frames / (med * 1e-3), 1)}), flush=True)
 
