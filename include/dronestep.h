@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 7
+#define DD_ABI_VERSION 8  /* 8: DD_ACT_PHILOX draws one block per 16 steps */
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
