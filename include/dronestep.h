@@ -302,8 +302,9 @@ enum { DD_MLP_F32 = 0, DD_MLP_F16X3 = 1 };
 
 /* Floats of a packed parameter buffer (same for K = 1 and 3, either compute). */
 int64_t dd_mlp_packed_floats(void);
-/* Repack state_dict tensors into `packed` (device, dd_mlp_packed_floats())
- * for `compute` (DD_MLP_*). */
+/* Repack state_dict tensors into `packed` (device, dd_mlp_packed_floats()
+ * floats, 16-byte aligned: every consumer reads it in 16-byte fragments;
+ * a misaligned pointer is hipErrorInvalidValue) for `compute` (DD_MLP_*). */
 int dd_mlp_pack(const DDMlpParams *params, int32_t compute, float *packed, void *stream);
 /* Forward pass; out_dim and compute must match the packed parameters. */
 int dd_mlp_forward(const float *packed, int32_t compute, int32_t out_dim,

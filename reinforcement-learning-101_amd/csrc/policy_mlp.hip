@@ -253,6 +253,7 @@ int64_t dd_mlp_packed_floats(void) { return dd::mlp::kPacked; }
 
 int dd_mlp_pack(const DDMlpParams* p, int32_t compute, float* packed, void* stream) {
     if (!p || !packed || !(p->out_dim == 1 || p->out_dim == 3) || !(p->ln_eps > 0.0f)) return hipErrorInvalidValue;
+    if (reinterpret_cast<uintptr_t>(packed) & 15u) return hipErrorInvalidValue;  // consumers read 16-byte fragments
     if (compute != DD_MLP_F32 && compute != DD_MLP_F16X3) return hipErrorInvalidValue;
     const float* req[] = {p->w0, p->b0, p->ln1_w, p->ln1_b, p->w3, p->b3, p->ln4_w,
                           p->ln4_b, p->w6, p->b6, p->ln7_w, p->ln7_b, p->w9, p->b9};
@@ -269,6 +270,7 @@ int dd_mlp_forward(const float* packed, int32_t compute, int32_t out_dim, const 
     if (compute != DD_MLP_F32 && compute != DD_MLP_F16X3) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
     if (!packed || !io->obs) return hipErrorInvalidValue;
+    if (reinterpret_cast<uintptr_t>(packed) & 15u) return hipErrorInvalidValue;  // 16-byte fragments / LDS-DMA
     if (out_dim == 1 && (io->actions || io->log_prob)) return hipErrorInvalidValue;  // nothing to sample
     const dd::mlp::FwdArgs a{io->obs, io->out, io->actions, io->log_prob, io->seed, io->step, io->env_id_base, n};
     const hipStream_t s = (hipStream_t)stream;

@@ -270,6 +270,7 @@ extern "C" int dd_policy_rollout(const DDConfig* cfg, const DDState* st, const f
     if (io->engine_reward && !io->shaped_hist) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
     if (!packed || !io->obs0 || (io->frames > 0 && (!io->reward || !io->done))) return hipErrorInvalidValue;
+    if (reinterpret_cast<uintptr_t>(packed) & 15u) return hipErrorInvalidValue;  // read as 16-byte fragments
     if (io->frames == 0 && io->obs_final == nullptr) return hipSuccess;
     dd::prl::Args p{};
     p.k = dd::make_consts(*cfg);

@@ -132,7 +132,7 @@ def test_policy_rollout_argument_errors_without_gpu():
     io.obs0 = io.reward = io.done = 8
     io.frames = 4
 
-    def run(state=None, packed=8, compute=abi.DD_MLP_F16X3, n=4, c=cfg):
+    def run(state=None, packed=16, compute=abi.DD_MLP_F16X3, n=4, c=cfg):
         st = state if state is not None else _state()
         return lib.dd_policy_rollout(ctypes.byref(c) if c is not None else None, ctypes.byref(st), packed, compute,
                                      ctypes.byref(io), n, None)
@@ -143,6 +143,7 @@ def test_policy_rollout_argument_errors_without_gpu():
     assert run(n=-1) == EINVAL
     assert run(compute=5) == EINVAL
     assert run(packed=None) == EINVAL
+    assert run(packed=8) == EINVAL  # packed parameters are read as 16-byte fragments
     io.obs0 = None
     assert run() == EINVAL  # frame 0's policy input is required
     io.obs0 = 8

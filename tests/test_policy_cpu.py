@@ -45,4 +45,8 @@ def test_forward_argument_errors_without_gpu():
         assert lib.dd_mlp_forward(None, mode, 3, ctypes.byref(io), 5, None) == 1    # null buffers
         assert lib.dd_mlp_pack(None, mode, None, None) == 1
     assert lib.dd_mlp_forward(None, 2, 3, ctypes.byref(io), 0, None) == 1           # bad compute
+    io.obs = 16
+    assert lib.dd_mlp_forward(ctypes.c_void_p(0x1008), abi.DD_MLP_F16X3, 3, ctypes.byref(io), 5, None) == 1
+    params = abi.DDMlpParams(*([16] * 14), 3, 1e-5)
+    assert lib.dd_mlp_pack(ctypes.byref(params), abi.DD_MLP_F16X3, ctypes.c_void_p(0x1004), None) == 1
     assert lib.dd_mlp_pack(None, 7, None, None) == 1
