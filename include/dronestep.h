@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 8  /* 8: DD_ACT_PHILOX draws one block per 16 steps */
+#define DD_ABI_VERSION 8  /* 8: DD_ACT_PHILOX draws one block per 32 steps */
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -61,9 +61,9 @@ enum {
                         /* the notebooks' Bernoulli(probs).sample() layout     */
     DD_ACT_U8X3 = 2,    /* uint8/bool[N][3] (main, left, right), nonzero = on */
     DD_ACT_PHILOX = 3   /* dd_rollout only: no action buffer; step s's
-                           bitmask is byte s & 15 of Philox4x32-10(key =
-                           action_seed, ctr = {env, s >> 4}) & 7 — a uniform
-                           random policy, one block per 16 steps            */
+                           bitmask is nibble s & 31 of Philox4x32-10(key =
+                           action_seed, ctr = {env, s >> 5}) & 7 — a uniform
+                           random policy, one block per 32 steps            */
 };
 
 /* Status byte bits (DDState.status). */

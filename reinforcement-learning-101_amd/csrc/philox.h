@@ -1,7 +1,7 @@
 // philox.h — Philox4x32-10 (Salmon et al., SC'11), the counter-based
 // generator behind every random draw on the device: spawns are keyed by
 // (seed; global env id, episode, 0), in-kernel random actions by
-// (seed; env id, step >> 4, 0xA5A5A5A5 ^ (step >> 4)_hi), one block per 16
+// (seed; env id, step >> 5, 0xA5A5A5A5 ^ (step >> 5)_hi), one block per 32
 // steps (drone_step.hip rollout_action), policy samples by
 // (seed; env id, step, 0x5A5A5A5A ^ step_hi).  Keyed by the global env id, a
 // lane's draws do not depend on sharding or launch geometry.

@@ -83,18 +83,18 @@ def test_rollout_without_obs_and_zero_frames(gpu_device):
 
 
 def philox_actions(seed, env0, n, step0, k):
-    """include/dronestep.h DD_ACT_PHILOX: step s's bitmask is byte s & 15 of
-    the Philox4x32-10 block (key seed; ctr env, s >> 4), low 3 bits."""
+    """include/dronestep.h DD_ACT_PHILOX: step s's bitmask is nibble s & 31 of
+    the Philox4x32-10 block (key seed; ctr env, s >> 5), low 3 bits."""
     key = [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF]
     out = np.zeros((k, n), dtype=np.uint8)
     for t in range(k):
         s = step0 + t
-        b = s >> 4
+        b = s >> 5
         for i in range(n):
             e = env0 + i
             ctr = [e & 0xFFFFFFFF, e >> 32, b & 0xFFFFFFFF, (b >> 32) ^ 0xA5A5A5A5]
-            word = ora.philox4x32_10(ctr, key)[(s >> 2) & 3]
-            out[t, i] = (word >> (8 * (s & 3))) & 7
+            word = ora.philox4x32_10(ctr, key)[(s >> 3) & 3]
+            out[t, i] = (word >> (4 * (s & 7))) & 7
     return out
 
 
@@ -105,8 +105,8 @@ def test_rollout_philox_policy(gpu_device):
     loop = VecDroneEnv(n, device=gpu_device, config=c, env_id_base=env0)
     roll.reset()
     loop.reset()
-    obs, reward, done = roll.rollout(frames=k, action_seed=77, action_step=40)
-    acts = torch.as_tensor(philox_actions(77, env0, n, 40, k), device=gpu_device)
+    obs, reward, done = roll.rollout(frames=k, action_seed=77, action_step=58)  # steps 58-69: two blocks
+    acts = torch.as_tensor(philox_actions(77, env0, n, 58, k), device=gpu_device)
     for t in range(k):
         o, r, d, _ = loop.step(acts[t])
         assert torch.equal(obs[t], o) and torch.equal(reward[t], r), t
@@ -115,9 +115,9 @@ def test_rollout_philox_policy(gpu_device):
 
 
 def test_rollout_philox_actions_do_not_depend_on_launch_split(gpu_device):
-    # 37 frames from step 5 (blocks of 16 steps: 0-15, 16-31, 32-47) as one launch
-    # and as launches of 9, 1, 14, 13 frames: the same actions, the same rollout
-    n, k = 200, 37
+    # 70 frames from step 5 (blocks of 32 steps: 0-31, 32-63, 64-95) as one launch
+    # and as launches of 9, 1, 27, 33 frames: the same actions, the same rollout
+    n, k = 200, 70
     c = EnvConfig(randomize_drone=True, auto_reset=True, seed=9)
     one = VecDroneEnv(n, device=gpu_device, config=c)
     split = VecDroneEnv(n, device=gpu_device, config=c)
@@ -125,7 +125,7 @@ def test_rollout_philox_actions_do_not_depend_on_launch_split(gpu_device):
     split.reset()
     obs, reward, done = one.rollout(frames=k, action_seed=3, action_step=5)
     parts, t0 = [], 0
-    for m in (9, 1, 14, 13):
+    for m in (9, 1, 27, 33):
         parts.append(split.rollout(frames=m, action_seed=3, action_step=5 + t0))
         t0 += m
     assert torch.equal(obs, torch.cat([q[0] for q in parts]))
