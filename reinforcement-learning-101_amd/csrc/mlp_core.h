@@ -177,7 +177,7 @@ __device__ __forceinline__ float add_other_half(float x) {
 // of registers hold adjacent rows, so the arithmetic runs as packed f32
 // (v_pk_add / v_pk_fma), in torch's form y = (x * rstd - rstd * mean) *
 // weight + bias.
-template <int NT, typename Emit>
+template <int NT, typename Emit, bool kBarrier = true>
 __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                Emit emit) {
     constexpr int kRows = 32 * NT;
@@ -224,7 +224,7 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
             y[r + 1] = fmaxf(v.y, 0.0f);
         }
         emit(t, y);
-        __builtin_amdgcn_sched_barrier(0);  // one tile's parameters in registers at a time
+        if constexpr (kBarrier) __builtin_amdgcn_sched_barrier(0);  // one tile's parameters in registers at a time
     }
 }
 
@@ -260,6 +260,66 @@ __device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const f
     });
 }
 
+// A no-op hook (mlp_body's mid, norm_split_cross's pre).
+struct NoMid {
+    __device__ void operator()() const {}
+};
+
+// norm_relu_split of a 128-row layer fused with the next layer's cross terms
+// (layer16's first loop): as soon as hidden tile t is split, the MFMAs of
+// k-steps 2t and 2t + 1 (which read only its fragments) are issued, so the
+// split of tile t + 1 can run in their shadow (a wave's own VALU does overlap
+// its own MFMAs; another wave's does not: tools/micro/mfma_valu_overlap.hip).
+// Each accumulator sees the same MFMAs in the same order as layer16's, so the
+// result is bit-identical; layer16_hihi finishes the layer.
+template <int NTO, typename Pre = NoMid>
+__device__ __forceinline__ void norm_split_cross(const f32x16 (&acc)[4], const float* vec, float eps, int h,
+                                                 const u32x4* __restrict__ a16n, int lane, f16x8 (&bh)[8],
+                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO], Pre pre = {}) {
+#pragma unroll
+    for (int to = 0; to < NTO; ++to)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) out[to][r] = 0.0f;
+    auto emit = [&](int t, const float (&v)[16]) {
+        split8(&v[0], bh[2 * t], bl[2 * t]);
+        split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
+        if (t == 0) pre();  // before the first read of the next layer's fragments
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int s = 2 * t + q;
+#pragma unroll
+            for (int to = 0; to < NTO; ++to) {
+                const u32x4* blk = a16n + (to * 8 + s) * 128;
+                const f16x8 ah = __builtin_bit_cast(f16x8, blk[lane]);
+                const f16x8 al = __builtin_bit_cast(f16x8, blk[64 + lane]);
+                out[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], out[to], 0, 0, 0);
+                out[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], out[to], 0, 0, 0);
+            }
+        }
+    };
+    norm_relu_emit<4, decltype(emit), false>(acc, vec, eps, h, emit);
+}
+
+// The rest of layer16 after its cross terms: scale them by 2^-11, add the
+// bias, accumulate the hi.hi products.
+template <int NT, int KS>
+__device__ __forceinline__ void layer16_hihi(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
+                                             f32x16 (&acc)[NT], const float* bias_h) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const f16x8 ah = __builtin_bit_cast(f16x8, a16[(t * KS + s) * 128 + lane]);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
 // as torch's Bernoulli does (probs_to_logits, clamp_probs): log p or
 // log(1 - p).  (torch evaluates it as -BCE-with-logits of the logit; the two
@@ -283,11 +343,10 @@ __device__ __forceinline__ float bernoulli_logp(float p, bool on) {
 // (kSplit, one k-step of 16), zero past column 14.  Every lane ends with z
 // of its column.  lds: the packed parameters.  mid() runs between layer 1
 // and layer 2 (dd_mlp_forward waits there for layers 2-3 of its LDS image).
-struct NoMid {
-    __device__ void operator()() const {}
-};
-
-template <int K, bool kSplit, typename Mid = NoMid>
+// kPipe: layer 2's split runs in the shadow of layer 3's cross-term MFMAs
+// (norm_split_cross, +16 VGPRs); the fused policy rollout, at the register
+// cap, takes the serial schedule.  Both give the same bits.
+template <int K, bool kSplit, bool kPipe = true, typename Mid = NoMid>
 __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float (&x)[8], float (&z)[K],
                                          Mid mid = {}) {
     const f32x4* lds4 = reinterpret_cast<const f32x4*>(lds);
@@ -304,8 +363,18 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
         norm_relu_split<4>(acc4, lds + kV1, eps, h, bh, bl);
         mid();
         layer16<4, 8>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
-        norm_relu_split<4>(acc4, lds + kV2, eps, h, bh, bl);
-        layer16<2, 8>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+#ifdef DD_MLP_SERIAL  // A/B: the serial schedule everywhere
+        constexpr bool kPipelined = false;
+#else
+        constexpr bool kPipelined = kPipe;
+#endif
+        if constexpr (kPipelined) {
+            norm_split_cross<2>(acc4, lds + kV2, eps, h, a16 + kA3 / 4, lane, bh, bl, acc2);
+            layer16_hihi<2, 8>(a16 + kA3 / 4, lane, bh, acc2, lds + kV3 + 4 * h);
+        } else {  // layer 2's LayerNorm + split, then all of layer 3
+            norm_relu_split<4>(acc4, lds + kV2, eps, h, bh, bl);
+            layer16<2, 8>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+        }
         norm_relu<2>(acc2, lds + kV3, eps, h, y3);
     } else {
         float y1[4][16], y2[4][16];

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
 
         // the actor and the collection loop's sampling (dd_mlp_forward)
         float z[3];
-        mlp::mlp_body<3, kSplit>(lds, lane, x, z);
+        mlp::mlp_body<3, kSplit, false>(lds, lane, x, z);  // serial schedule: the frame holds the registers
         float prob[3];
         mlp::actor_probs(z, prob);
         uint32_t act;

@@ -68,6 +68,40 @@ __device__ __forceinline__ void valu_scalar_work(int v, float* sink, int lane) {
     if (s == 1234.5f) sink[lane] = s;
 }
 
+// The MFMA and VALU work of one wave in one loop: each round 4 independent
+// MFMAs with vpr x 8 independent packed FMAs placed between them
+// (sched_group_barrier: 1 MFMA, 2 * vpr VALU, four times).
+template <int VPR>
+__device__ __forceinline__ void mixed_work(int m, float* sink, int lane) {
+    f16x8 a = {(_Float16)1, (_Float16)lane, 0, 0, 0, 0, 0, (_Float16)0.5f};
+    f16x8 b = a;
+    f32x16 acc[4] = {};
+    f32x2 x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = f32x2{(float)lane * 1e-3f + j, 1.0f - j};
+    const f32x2 c = {0.999f, 0.999f}, d = {1e-4f, 2e-4f};
+    for (int i = 0; i < m; ++i) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < VPR; ++q) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = __builtin_elementwise_fma(x[j], c, d);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);        // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2 * VPR, 0);  // its share of the VALU
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) s += acc[t][0] + acc[t][15];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += x[j].x + x[j].y;
+    if (s == 1234.5f) sink[lane] = s;
+}
+
 // mode 0: MFMA waves only; 1: VALU waves only; 2: both, in different waves;
 // 3: both in the same waves (waves 0-3 do MFMA then VALU in one stream);
 // 4: VALU waves only, as scalar v_fma_f32; 5 / 6: packed / scalar VALU in all 8 waves
@@ -85,6 +119,11 @@ __global__ __launch_bounds__(512) void k(int mode, int m, int v, float* sink) {
     }
     if (mode == 5 && wave < 4) valu_work(v, sink, lane);   // packed, both waves of a SIMD
     if (mode == 6) valu_scalar_work(v, sink, lane);         // scalar, both waves of a SIMD
+    if ((mode == 7 && wave < 4) || mode == 8) {  // interleaved in one wave (7) / in both waves of a SIMD (8)
+        if (v == m) mixed_work<1>(m, sink, lane);
+        else if (v == 2 * m) mixed_work<2>(m, sink, lane);
+        else mixed_work<4>(m, sink, lane);
+    }
 }
 
 int main() {
@@ -97,7 +136,7 @@ int main() {
     const int m = 2000, vs[] = {2000, 4000, 8000};
     for (int vi = 0; vi < 3; ++vi) {
         const int v = vs[vi];
-        for (int mode = 0; mode < 7; ++mode) {
+        for (int mode = 0; mode < 9; ++mode) {
             float best = 1e30f;
             for (int r = 0; r < 5; ++r) {
                 CK(hipEventRecord(e0));
