@@ -260,7 +260,7 @@ __device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const f
     });
 }
 
-// A no-op hook (mlp_body's mid, norm_split_cross's pre).
+// A no-op hook (mlp_body's mid).
 struct NoMid {
     __device__ void operator()() const {}
 };
@@ -272,10 +272,10 @@ struct NoMid {
 // its own MFMAs; another wave's does not: tools/micro/mfma_valu_overlap.hip).
 // Each accumulator sees the same MFMAs in the same order as layer16's, so the
 // result is bit-identical; layer16_hihi finishes the layer.
-template <int NTO, typename Pre = NoMid>
+template <int NTO>
 __device__ __forceinline__ void norm_split_cross(const f32x16 (&acc)[4], const float* vec, float eps, int h,
                                                  const u32x4* __restrict__ a16n, int lane, f16x8 (&bh)[8],
-                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO], Pre pre = {}) {
+                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO]) {
 #pragma unroll
     for (int to = 0; to < NTO; ++to)
 #pragma unroll
@@ -283,7 +283,6 @@ __device__ __forceinline__ void norm_split_cross(const f32x16 (&acc)[4], const f
     auto emit = [&](int t, const float (&v)[16]) {
         split8(&v[0], bh[2 * t], bl[2 * t]);
         split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
-        if (t == 0) pre();  // before the first read of the next layer's fragments
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int s = 2 * t + q;
