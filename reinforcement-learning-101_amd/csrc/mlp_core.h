@@ -72,14 +72,25 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 // (v_cvt_pk_f16_f32).  a - hi is exact in f32 (hi is a to 11 bits), the
 // scaling by 2^11 too.  (Truncating instead, v_cvt_pkrtz, biases lo' and
 // quadruples the end-to-end error: tools/mlp_split_sim.py --truncate.)
-// Written on float pairs so it lowers to v_cvt_pk_f16_f32, two
-// v_cvt_f32_f16, v_pk_add_f32, v_pk_mul_f32, v_cvt_pk_f16_f32 (6 VALU per
-// pair; scalar code had the compiler convert each half twice: 10).
+// The residual (a - hi) 2^11 is one v_fma_mix_f32 per element,
+// fma(-hi, 2^11, a 2^11) with hi read as f16 straight from the packed
+// register (exact: the product and the sum are exact, so the one rounding
+// changes nothing): v_cvt_pk_f16_f32, v_pk_mul_f32, two v_fma_mix_f32,
+// v_cvt_pk_f16_f32 = 5 VALU per pair, the same bits as converting hi back to
+// f32 and subtracting (6; -DDD_MLP_SPLIT_CVT, tools/mlp_equal_check.py).
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
     uint32_t hp = __builtin_bit_cast(uint32_t, f16x2{(_Float16)a, (_Float16)b});
     asm("" : "+v"(hp));  // widen hi from the packed register (else each half is converted twice)
+#ifdef DD_MLP_SPLIT_CVT
     const f16x2 h = __builtin_bit_cast(f16x2, hp);
     const f32x2 r = (f32x2{a, b} - f32x2{(float)h.x, (float)h.y}) * f32x2{kLoScale, kLoScale};
+#else
+    const f32x2 as = f32x2{a, b} * f32x2{kLoScale, kLoScale};
+    f32x2 r;
+    asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r.x) : "v"(hp), "v"(kLoScale), "v"(as.x));
+    asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r.y) : "v"(hp), "v"(kLoScale),
+        "v"(as.y));
+#endif
     const f16x2 l = {(_Float16)r.x, (_Float16)r.y};
     hi = hp;
     lo = __builtin_bit_cast(uint32_t, l);

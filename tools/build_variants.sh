@@ -59,6 +59,7 @@ for v in ${VARIANTS:-base}; do
     mpad*) build $v -DDD_MLP_PAD=${v#mpad} ;;
     log1p) build log1p -DDD_MLP_LOG1P ;;
     serial) build serial -DDD_MLP_SERIAL ;;
+    splitcvt) build splitcvt -DDD_MLP_SPLIT_CVT ;;
     uncentered) build uncentered -DDD_MLP_UNCENTERED ;;
     tl_s*_o*)  # timeline + store policies: tl_s<state>_o<out and obs>, values as DD_ST_* (>= 100: raw aux bits)
       s=${v#tl_s}; s=${s%%_o*}; o=${v##*_o}
