@@ -1,0 +1,76 @@
+#!/bin/bash
+# One launcher for GPU-box sessions (run through gpurun from the repo root):
+#
+#   bash tools/gpu.sh <tag> <step> [<step> ...]
+#
+# Steps run in the order given, each under its own time limit, and the first
+# failure ends the session (a fault, abort or time-out starts nothing more on
+# the GPU).  Output goes to gpurun_out/<tag>/.
+#
+#   tests      pytest -m gpu (PYTEST_ARGS adds options, e.g. -k)
+#   smoke      __graft_entry__.smoke()
+#   bench20    the driver's line: bench.py --gpus 1 --steps 20 --warmup 5
+#   bench      bench.py with its defaults (every extra point)
+#   prof       rocprofv3 kernel traces: config 3, the 16.8M HBM point, the extra points
+#   pmc        FETCH_SIZE / WRITE_SIZE passes of the step kernel at 262,144 and 16.8M drones
+#   sq         SQ instruction counters of the step / rollout kernels (tools/pmc_sq.sh)
+#   lab        tools/kernel_lab.py (VARIANTS, ENVS, LABARGS)
+#   py:<file>  python <file> (LABARGS passed through), output in <tag>/<file stem>.log
+set -o pipefail
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+
+run_step() {
+    case "$1" in
+    tests)
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} \
+            > $OUT/pytest_gpu.log 2>&1; local rc=$?; tail -2 $OUT/pytest_gpu.log; return $rc ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; local rc=$?
+        tail -1 $OUT/smoke.log; return $rc ;;
+    bench20)
+        timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_k20.json 2> $OUT/bench_k20.err \
+            && cat $OUT/bench_k20.json ;;
+    bench)
+        timeout -k 10 600 python bench.py ${BENCHARGS} > $OUT/bench_default.json 2> $OUT/bench_default.err \
+            && python3 tools/bench_summary.py $OUT/bench_default.json ;;
+    prof)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3 -o bench -f csv -- python3 bench.py \
+            --steps 2000 --warmup 200 --cpu-baseline 0 --hbm-point 0 --rollout-point 0 --no-extra-points \
+            > $OUT/prof_c3_bench.json 2> $OUT/prof.err &&
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_16m -o bench -f csv -- python3 bench.py \
+            --envs-per-gpu 16777216 --steps 200 --warmup 20 --cpu-baseline 0 --hbm-point 0 --rollout-point 0 \
+            --no-extra-points > $OUT/prof_16m_bench.json 2>> $OUT/prof.err &&
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_extra -o bench -f csv -- python3 bench.py \
+            --steps 200 --warmup 20 --cpu-baseline 0 --hbm-point 0 > $OUT/prof_extra_bench.json 2>> $OUT/prof.err ;;
+    pmc)
+        for N in 262144 16777216; do
+            for C in FETCH_SIZE WRITE_SIZE; do
+                timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex step_kernel -d $OUT/pmc_${C}_$N -o pmc \
+                    -f csv -- python3 bench.py --envs-per-gpu $N --steps 50 --warmup 5 --graph-steps 0 \
+                    --cpu-baseline 0 --hbm-point 0 --rollout-point 0 --no-extra-points > /dev/null 2>> $OUT/pmc.err \
+                    || return 1
+            done
+        done ;;
+    sq)
+        bash tools/pmc_sq.sh $OUT ;;
+    lab)
+        timeout -k 10 600 python tools/kernel_lab.py --variants ${VARIANTS:-base} --envs ${ENVS:-262144,1048576,16777216} \
+            ${LABARGS} > $OUT/lab.jsonl 2> $OUT/lab.err; local rc=$?; cat $OUT/lab.jsonl; tail -5 $OUT/lab.err; return $rc ;;
+    py:*)
+        local f=${1#py:}; local stem=$(basename ${f%.py})
+        timeout -k 10 ${PYTIMEOUT:-600} python -u $f ${LABARGS} > $OUT/$stem.log 2>&1; local rc=$?
+        tail -${PYTAIL:-20} $OUT/$stem.log; return $rc ;;
+    *)
+        echo "unknown step $1"; return 2 ;;
+    esac
+}
+
+for step in "$@"; do
+    echo "== $step"
+    run_step "$step" || { echo "== step $step failed (rc=$?); stopping"; exit 1; }
+done
+echo "== done"
