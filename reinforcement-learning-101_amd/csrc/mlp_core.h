@@ -42,9 +42,27 @@ constexpr int kV2 = kV1 + 3 * 128;
 constexpr int kV3 = kV2 + 3 * 128;  // [3][64]
 constexpr int kW4 = kV3 + 3 * 64;   // last layer [3][64], rows >= K zero
 constexpr int kB4 = kW4 + 3 * 64;   // bias [3], LayerNorm eps
-constexpr int kPacked = kB4 + 4;
+constexpr int kTag = kB4 + 4;       // layout tag [4]: pack_tag(compute, K), then zeros
+constexpr int kPacked = kTag + 4;
 constexpr size_t kLdsBytes = kPacked * sizeof(float);
 static_assert(kPacked % 4 == 0, "packed buffer is read as float4");
+
+// What dd_mlp_pack wrote the buffer for: the A sections' arithmetic
+// (DD_MLP_*) and the output width K, as the payload of a quiet NaN.
+__host__ __device__ constexpr uint32_t pack_tag(int compute, int out_dim) {
+    return 0x7FC0DD00u | ((uint32_t)compute << 4) | (uint32_t)out_dim;
+}
+
+// Float4 i of the packed buffer on its way into LDS.  The fragment holding
+// the LayerNorm eps carries a NaN eps when the buffer's tag is not the
+// launch's (packed for another compute or K): every LayerNorm, hence every
+// probability, log-probability and value, comes out NaN instead of numbers
+// from misread weights.
+__device__ __forceinline__ f32x4 packed_fragment(const f32x4* src4, int i, uint32_t tag) {
+    f32x4 v = src4[i];
+    if (i == kB4 / 4 && __float_as_uint(src4[kTag / 4].x) != tag) v.w = __builtin_nanf("");
+    return v;
+}
 
 // The three hidden Linears are packed mean-centred over their outputs
 // (policy_mlp.hip weight_at), so the LayerNorm that follows each skips its

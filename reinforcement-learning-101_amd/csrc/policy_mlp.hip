@@ -126,9 +126,11 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
     } else if (i < kB4) {
         const int o = i - kW4;
         v = (o / 64) < p.out_dim ? p.w9[o] : 0.0f;
-    } else {
+    } else if (i < kTag) {
         const int o = i - kB4;
         v = o < p.out_dim ? p.b9[o] : (o == 3 ? p.ln_eps : 0.0f);
+    } else {
+        v = i == kTag ? __uint_as_float(pack_tag(compute, p.out_dim)) : 0.0f;
     }
     out[i] = v;
 }
@@ -179,7 +181,8 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
     load_inputs<kSplit>(p, tile, lane, x);
     const f32x4* src4 = reinterpret_cast<const f32x4*>(packed);
     for (int i = threadIdx.x; i < kA2 / 4; i += kThreads) lds4[i] = src4[i];
-    for (int i = kV1 / 4 + threadIdx.x; i < kPacked / 4; i += kThreads) lds4[i] = src4[i];
+    for (int i = kV1 / 4 + threadIdx.x; i < kPacked / 4; i += kThreads)
+        lds4[i] = packed_fragment(src4, i, pack_tag(kSplit ? DD_MLP_F16X3 : DD_MLP_F32, K));
     asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
     constexpr int kChunk = 64 * 4;  // floats per wave-instruction
     static_assert((kV1 - kA2) % kChunk == 0 && kA2 % kChunk == 0, "DMA chunks");
@@ -227,13 +230,11 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
 
 template <int K, bool kSplit>
 hipError_t launch(const float* packed, const FwdArgs& a, hipStream_t s) {
-    static bool configured = false;  // the LDS image exceeds the 64 KB default
-    if (!configured) {
-        const hipError_t e = hipFuncSetAttribute((const void*)mlp_kernel<K, kSplit>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
-        if (e != hipSuccess) return e;
-        configured = true;
-    }
+    // the LDS image exceeds the 64 KB default; the attribute is per device, so
+    // it is set on every launch (a cheap host call) rather than once per process
+    const hipError_t e = hipFuncSetAttribute((const void*)mlp_kernel<K, kSplit>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+    if (e != hipSuccess) return e;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;

@@ -124,7 +124,9 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
                                                                   Soa<T> a) {
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
-    for (int i = threadIdx.x; i < kPacked / 4; i += kThreads) lds4[i] = reinterpret_cast<const f32x4*>(packed)[i];
+    for (int i = threadIdx.x; i < kPacked / 4; i += kThreads)
+        lds4[i] = mlp::packed_fragment(reinterpret_cast<const f32x4*>(packed), i,
+                                       mlp::pack_tag(kSplit ? DD_MLP_F16X3 : DD_MLP_F32, 3));
     __syncthreads();  // the only block barrier: waves run their frames independently
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
@@ -240,13 +242,10 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
 
 template <typename T, bool kSplit, bool kRef>
 hipError_t launch(const float* packed, const Args& p, const Soa<T>& a, hipStream_t s) {
-    static bool configured = false;  // the LDS image exceeds the 64 KB default
-    if (!configured) {
-        const hipError_t e = hipFuncSetAttribute((const void*)policy_rollout_kernel<T, kSplit, kRef>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
-        if (e != hipSuccess) return e;
-        configured = true;
-    }
+    // the LDS image exceeds the 64 KB default; per device, so set on every launch
+    const hipError_t e = hipFuncSetAttribute((const void*)policy_rollout_kernel<T, kSplit, kRef>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+    if (e != hipSuccess) return e;
     const int64_t tiles = (p.n + kCols - 1) / kCols;
     const unsigned blocks = (unsigned)((tiles + kWaves - 1) / kWaves);  // one wave per 32-drone tile
     hipLaunchKernelGGL((policy_rollout_kernel<T, kSplit, kRef>), dim3(blocks), dim3(kThreads), kLdsBytes, s, packed,

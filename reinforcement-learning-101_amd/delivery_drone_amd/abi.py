@@ -20,7 +20,7 @@ __all__ = [
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 8
+DD_ABI_VERSION = 9
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8

@@ -11,8 +11,9 @@ with K = 3 + Sigmoid for the actor and K = 1 for the critic.  A
 ``torch.load(path, weights_only=True)``), packs it once into the kernel's
 MFMA operand order, and evaluates N observation rows per call in float32
 (``compute="f32"``, the default) or with the hidden GEMMs on the f16 MFMA as
-split hi/lo operand pairs (``compute="f16x3"``: about 4x faster, about the
-same end-to-end error; include/dronestep.h ``DD_MLP_F16X3``).
+split hi/lo operand pairs (``compute="f16x3"``: about 2x faster — 65,536 rows
+35.8 -> 15-18 us on MI355X — about the same end-to-end error;
+include/dronestep.h ``DD_MLP_F16X3``).
 The actor also does the collection loop's ``Bernoulli(probs).sample()`` and
 ``.log_prob(actions).sum(dim=1)`` (:857-859) in the same launch, returning the
 actions as the ``dd_step`` bitmask, so a policy-driven rollout never leaves
@@ -74,6 +75,16 @@ class MlpNet:
         # keep the source tensors alive until the pack kernel has read them
         self._src = {k: torch.as_tensor(sd[k]).detach().to(device=self.device, dtype=torch.float32).contiguous()
                      for k in STATE_DICT_KEYS}
+        if compute == "f16x3":
+            # the hidden Linears' weights go into f16 halves after centring over
+            # their outputs (|w - mean| <= 2 max|w|): beyond the f16 range the hi
+            # half is inf and every probability NaN, so refuse such weights here
+            # (observations and activations must stay below 65504 as well)
+            for k in ("0.weight", "3.weight", "6.weight"):
+                w = self._src[k]
+                if not bool(torch.isfinite(w).all()) or float(w.abs().max()) >= 65504.0 / 2:
+                    raise ValueError(f"{k}: compute='f16x3' needs finite weights below 32752 in magnitude "
+                                     "(the f16 range after centring); use compute='f32'")
         p = abi.DDMlpParams(*[self._src[k].data_ptr() for k in STATE_DICT_KEYS], self.out_dim, self.ln_eps)
         self.packed = torch.empty(int(self._lib.dd_mlp_packed_floats()), dtype=torch.float32, device=self.device)
         abi.check(self._lib.dd_mlp_pack(ctypes.byref(p), self._mode, self.packed.data_ptr(), self._stream()),

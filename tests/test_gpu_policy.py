@@ -179,3 +179,51 @@ def test_f16x3_tracks_f32(fixture, gpu_device):
     obs = torch.cat([torch.as_tensor(d["obs"], device=gpu_device),
                      torch.randn(4096, 15, device=gpu_device) * 10.0])
     close(a16(obs).cpu().numpy(), a32(obs).cpu().numpy(), 0.0, 3e-6)
+
+
+def test_packed_layout_tag_poisons_mismatched_launches(fixture, gpu_device):
+    # a buffer packed for one compute / K and run as another gives NaN, not
+    # numbers from misread weights; the right pairing stays finite
+    from delivery_drone_amd import abi
+    import ctypes
+    d, nets = fixture
+    obs = torch.as_tensor(d["obs"], device=gpu_device)
+    n = obs.shape[0]
+    lib = abi.lib()
+    for compute, other in (("f32", abi.DD_MLP_F16X3), ("f16x3", abi.DD_MLP_F32)):
+        actor = MlpNet(nets["actor"], device=gpu_device, compute=compute)
+        critic = MlpNet(nets["critic"], device=gpu_device, compute=compute)
+        probs = torch.empty(n, 3, device=gpu_device)
+        lp = torch.empty(n, device=gpu_device)
+        io = abi.DDMlpIO(obs.data_ptr(), probs.data_ptr(), None, lp.data_ptr(), 0, 0, 0)
+        abi.check(lib.dd_mlp_forward(actor.packed.data_ptr(), other, 3, ctypes.byref(io), n, None), "fwd")
+        torch.cuda.synchronize()
+        assert bool(torch.isnan(probs).all()) and bool(torch.isnan(lp).all())
+        vals = torch.empty(n, device=gpu_device)
+        io = abi.DDMlpIO(obs.data_ptr(), vals.data_ptr(), None, None, 0, 0, 0)
+        abi.check(lib.dd_mlp_forward(actor.packed.data_ptr(), actor._mode, 1, ctypes.byref(io), n, None), "fwd")
+        torch.cuda.synchronize()
+        assert bool(torch.isnan(vals).all())  # an actor buffer run as a critic
+        io = abi.DDMlpIO(obs.data_ptr(), vals.data_ptr(), None, None, 0, 0, 0)
+        abi.check(lib.dd_mlp_forward(critic.packed.data_ptr(), critic._mode, 1, ctypes.byref(io), n, None), "fwd")
+        torch.cuda.synchronize()
+        assert bool(torch.isfinite(vals).all())
+        # dd_policy_rollout with a critic's buffer: NaN log-probabilities
+        env = VecDroneEnv(64, device=gpu_device, randomize_drone=True)
+        env.reset()
+        critic.out_dim = 3  # get past the wrapper's own check to reach the C ABI
+        _, _, lp2, _, _ = env.policy_rollout(critic, 3)
+        torch.cuda.synchronize()
+        assert bool(torch.isnan(lp2).all())
+        _, _, lp3, _, _ = env.policy_rollout(actor, 3)
+        assert bool(torch.isfinite(lp3).all())
+
+
+def test_f16x3_refuses_weights_beyond_f16_range(fixture, gpu_device):
+    _, nets = fixture
+    sd = {k: np.array(v, copy=True) for k, v in nets["actor"].items()}
+    key = next(k for k in sd if k.endswith("3.weight"))
+    sd[key][0, 0] = 40000.0
+    with pytest.raises(ValueError, match="f16"):
+        MlpNet(sd, device=gpu_device, compute="f16x3")
+    MlpNet(sd, device=gpu_device, compute="f32")  # f32 takes them

@@ -168,3 +168,41 @@ def test_policy_rollout_default_devices(gpu_device):
         obs, acts, lp, rew, done = env.policy_rollout(actor_, 3)
     assert actor_.device == env.device
     assert obs.shape == (3, 96, 15) and acts.shape == (3, 96) and bool(torch.isfinite(lp).all())
+
+
+@pytest.mark.parametrize("before", ["rollout", "step_no_obs", "step_out", "load_state"])
+def test_policy_rollout_after_paths_that_leave_obs_stale(before, gpu_device):
+    # rollout(), step(write_obs=False), step(out=...) and load_state_dict() move the
+    # lanes without refreshing env.obs; policy_rollout's frame 0 must still see the
+    # current state's observation (a stale obs0 went unnoticed)
+    n, frames = 777, 40
+    net = actor(gpu_device, 2, "f16x3")
+    fused, ref = twins(n, gpu_device, randomize_drone=True, auto_reset=True, seed=9)
+    for env in (fused, ref):
+        g = torch.Generator(device=gpu_device).manual_seed(3)
+        acts = torch.randint(0, 8, (12, n), device=gpu_device, generator=g, dtype=torch.uint8)
+        if before == "rollout":
+            env.rollout(acts)
+        elif before == "step_no_obs":
+            for t in range(12):
+                env.step(acts[t], write_obs=False)
+        elif before == "step_out":
+            o = torch.empty(n, 15, device=gpu_device)
+            r = torch.empty(n, device=gpu_device)
+            d = torch.empty(n, dtype=torch.bool, device=gpu_device)
+            for t in range(12):
+                env.step(acts[t], out=(o, r, d))
+        else:
+            other = VecDroneEnv(n, device=gpu_device, config=env.config)
+            other.reset()
+            other.rollout(acts)
+            env.load_state_dict(other.state_dict())
+    ref.get_state()  # the loop reads the refreshed observation explicitly
+    obs, acts, lp, rew, done = fused.policy_rollout(net, frames, seed=1, step=0)
+    r_obs, r_acts, r_lp, r_rew, r_done, _, _ = loop(ref, net, frames, 1, 0)
+    assert torch.equal(obs, r_obs)
+    assert torch.equal(acts, r_acts)
+    assert torch.equal(lp, r_lp)
+    assert torch.equal(rew, r_rew)
+    assert torch.equal(done, r_done)
+    assert_same_state(fused, ref)

@@ -29,7 +29,7 @@ def test_log_prob_fixture_is_bernoulli_sum():
 def test_packed_size_and_exports():
     lib = abi.lib()
     # A operands 2048 + 16384 + 8192, vectors 3*(128+128+64), last layer 192, bias + eps 4
-    assert lib.dd_mlp_packed_floats() == 2048 + 16384 + 8192 + 960 + 192 + 4
+    assert lib.dd_mlp_packed_floats() == 2048 + 16384 + 8192 + 960 + 192 + 4 + 4  # ... bias+eps, layout tag
     for name in ("dd_mlp_pack", "dd_mlp_forward"):
         assert hasattr(lib, name)
 
