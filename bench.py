@@ -43,8 +43,10 @@ def parse():
     p.add_argument("--graph-steps", type=int, default=50, help="launches per captured hipGraph (0 = eager)")
     p.add_argument("--no-obs", action="store_true", help="skip the observation write (not the default)")
     p.add_argument("--action-rows", type=int, default=64, help="distinct pre-generated action rows cycled")
-    p.add_argument("--cpu-baseline", type=float, default=10.0, help="seconds of CPU-baseline wall time (0 = skip)")
-    p.add_argument("--cpu-workers", type=int, default=0, help="CPU-baseline processes (0 = min(16, cpus))")
+    p.add_argument("--cpu-baseline", type=float, default=8.0,
+                   help="seconds of CPU-baseline wall time per leg (0 = skip)")
+    p.add_argument("--cpu-workers", type=int, default=0,
+                   help="CPU-baseline processes per leg (0 = min(16, CPUs in this process's affinity))")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
@@ -61,48 +63,75 @@ def parse():
 
 # ----------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
-    lane0, lanes, steps, seed = args
+    leg, lane0, lanes, steps, seed = args
     from delivery_drone_amd.config import EnvConfig
     from oracle import oracle as ora
-    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    from oracle import pyloop
     t0 = time.perf_counter()
-    chk = ora.bench(cfg, lane0, lanes, steps)
+    if leg == "python_objects":
+        _, chk = pyloop.bench(lane0, lanes, steps, seed)
+    else:
+        cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+        chk = ora.bench(cfg, lane0, lanes, steps)
     return time.perf_counter() - t0, chk
 
 
-def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
-    """The fixture-pinned C restatement of DroneGame.step (oracle/) on the
-    host's cores, config-3 workload (random spawn, auto-reset, random actions,
-    obs built every frame), a bounded sample sized to ~`seconds` of wall."""
-    from oracle import oracle as ora
-    ora.build()
-    lanes = 16_384
-    calib_steps = 20
-    dt, _ = _cpu_worker((0, lanes, calib_steps, seed))
+def _cpu_leg(leg: str, seconds: float, workers: int, seed: int, lanes: int, calib_steps: int) -> dict:
+    dt, _ = _cpu_worker((leg, 0, lanes, calib_steps, seed))
     per_lane_step = dt / (lanes * calib_steps)
     steps = max(1, int(seconds / (per_lane_step * lanes)))
     ctx = mp.get_context("fork")  # before any GPU call in this process
-    jobs = [(w * lanes, lanes, steps, seed) for w in range(workers)]
+    jobs = [(leg, w * lanes, lanes, steps, seed) for w in range(workers)]
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
         res = pool.map(_cpu_worker, jobs)
     wall = time.perf_counter() - t0
-    total = workers * lanes * steps
     if not all(math.isfinite(c) for _, c in res):
-        raise RuntimeError("CPU baseline produced a non-finite checksum")
+        raise RuntimeError(f"CPU baseline leg {leg} produced a non-finite checksum")
+    total = workers * lanes * steps
+    return {"value": round(total / wall, 1), "per_core": round(total / wall / workers, 1),
+            "single_process": round(1.0 / per_lane_step, 1), "workers": workers, "drones_per_worker": lanes,
+            "frames": steps, "drone_steps": total, "wall_s": round(wall, 2)}
+
+
+def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
+    """The reference's step on the host's cores, config-3 workload (random
+    spawn, auto-reset, uniform random actions, observation every frame), a
+    bounded sample of ~`seconds` per leg:
+
+    * python_objects (the value): oracle/pyloop.py, one Python game object
+      per drone shaped like DroneGame.step (game_engine.py:95-138) with numpy
+      scalar trig and pow squares, pinned bit for bit to the reference's
+      fixtures (tests/test_pyloop.py) — the reference loop's own speed;
+    * c_scalar: oracle/drone_oracle.c, the fixture-pinned scalar f64 C
+      restatement (what a native CPU port reaches).
+
+    `workers` processes per leg (default: the CPUs this process may run on,
+    capped at 16 — the GPU box's CPU share per GPU; --cpu-workers overrides)."""
+    from oracle import oracle as ora
+    ora.build()
+    legs = {"python_objects": _cpu_leg("python_objects", seconds, workers, seed, 256, 8),
+            "c_scalar": _cpu_leg("c_scalar", seconds, workers, seed, 16_384, 20)}
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except (OSError, IndexError):
         model = platform.processor()
+    py, c = legs["python_objects"], legs["c_scalar"]
     return {
-        "value": total / wall,
+        "value": py["value"],
         "unit": "env-steps/s",
         "cores": workers,
         "kind": "port",
-        "sample": (f"oracle/drone_oracle.c (fixture-pinned scalar f64 restatement of DroneGame.step + "
-                   f"get_state), config-3 workload: {workers} processes x {lanes} drones x {steps} frames "
-                   f"= {total:.3g} drone-steps in {wall:.1f} s on {model}; single-process "
-                   f"{1.0 / per_lane_step:.3g} steps/s"),
+        "host_cores": os.cpu_count(),
+        "affinity_cores": len(os.sched_getaffinity(0)),
+        "cpu_model": model,
+        "legs": legs,
+        "sample": (f"config-3 workload, {workers} processes per leg on {model} (host: {os.cpu_count()} CPUs, "
+                   f"{len(os.sched_getaffinity(0))} in this process's affinity). value = python_objects: "
+                   f"oracle/pyloop.py (DroneGame.step-shaped Python objects, fixture-pinned), {py['drone_steps']:.3g} "
+                   f"drone-steps in {py['wall_s']} s, {py['per_core']:.3g} per core; c_scalar: "
+                   f"oracle/drone_oracle.c, {c['drone_steps']:.3g} drone-steps in {c['wall_s']} s, "
+                   f"{c['per_core']:.3g} per core"),
     }
 
 
@@ -577,7 +606,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline > 0:
-        workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+        workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))
         cpu = cpu_baseline(args.cpu_baseline, workers, args.seed)
 
     import torch
@@ -705,6 +734,7 @@ def main():
         value = total_steps / wall
         step_ms = gpu_ms / args.steps  # device time per launch on the kernel's stream
         bytes_env = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=write_obs)
+        traffic, traffic_note = pmc_traffic_row(n, args.precision, write_obs)
         achieved = bytes_env * n / (step_ms * 1e-3) / 1e9
         roof = {
             "bound": "hbm",
@@ -712,7 +742,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(n, args.precision, write_obs),
+            "traffic": traffic,
+            "traffic_note": traffic_note,
             "bytes_per_env": bytes_env,
             "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, false>",
             "timing": "HIP events on the launch stream over the K timed steps / K",
@@ -762,6 +793,7 @@ def main():
             "render_point": rp,
             "gpu_ms_per_step": round(step_ms, 6),
             "device": torch.cuda.get_device_name(dev),
+            "build_info": abi.lib().dd_build_info().decode(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -769,18 +801,33 @@ def main():
 
 
 def pmc_traffic(n: int, precision: str, obs: bool):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, produced by tools/profile.sh), or None."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    """HBM bytes per launch of the step kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, tools/pmc_summary.py), or None.  A row
+    counts only if it was measured on this very build: its build_info (ABI
+    version + step-kernel ISA hash) must equal the loaded library's."""
+    return pmc_traffic_row(n, precision, obs)[0]
+
+
+def pmc_traffic_row(n: int, precision: str, obs: bool, path: str | None = None):
+    """(bytes or None, note) — the note says why a row was not taken."""
+    from delivery_drone_amd import abi
+    path = path or os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             rows = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no profiles/pmc_traffic.json"
+    have = abi.lib().dd_build_info().decode()
+    step_isa = dict(kv.split("=", 1) for kv in have.split(";")).get("step_isa")
     for r in rows.get("rows", []):
         if r.get("envs") == n and r.get("precision") == precision and r.get("obs") == obs:
-            return r.get("hbm_bytes_per_launch")
-    return None
+            got = r.get("build_info")
+            if not got:
+                return None, "PMC row has no build_info (measured on an older build)"
+            if dict(kv.split("=", 1) for kv in got.split(";")).get("step_isa") != step_isa:
+                return None, f"PMC row measured on step_isa of '{got}', this library is '{have}'"
+            return r.get("hbm_bytes_per_launch"), f"PMC FETCH_SIZE/WRITE_SIZE passes on build {got}"
+    return None, f"no PMC row for envs={n} precision={precision} obs={obs}"
 
 
 if __name__ == "__main__":

@@ -379,6 +379,10 @@ int64_t dd_step_bytes_per_env(int32_t precision, int32_t action_format,
 
 const char *dd_error_string(int code);
 int dd_abi_version(void);
+/* "abi=<n>;step_isa=<sha256/16>;policy_rollout_isa=<sha256/16>": the ABI version
+ * and hashes of the device ISA this library was built with (tools/build_info.py);
+ * bench.py reports PMC traffic only for the build it was measured on. */
+const char *dd_build_info(void);
 
 #ifdef __cplusplus
 }

@@ -68,8 +68,8 @@ def _p(a):
 
 
 def philox4x32_10(ctr, key):
-    c = np.asarray(ctr, dtype=np.uint32)
-    k = np.asarray(key, dtype=np.uint32)
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
     out = np.zeros(4, dtype=np.uint32)
     lib().ora_philox4x32_10(_p(c), _p(k), _p(out))
     return out

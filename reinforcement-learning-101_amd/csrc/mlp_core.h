@@ -54,13 +54,17 @@ __host__ __device__ constexpr uint32_t pack_tag(int compute, int out_dim) {
 }
 
 // Float4 i of the packed buffer on its way into LDS.  The fragment holding
-// the LayerNorm eps carries a NaN eps when the buffer's tag is not the
-// launch's (packed for another compute or K): every LayerNorm, hence every
-// probability, log-probability and value, comes out NaN instead of numbers
-// from misread weights.
+// the last layer's bias and the LayerNorm eps arrives as NaNs when the
+// buffer's tag is not the launch's (packed for another compute or K): every
+// output (probability, log-probability, value) comes out NaN instead of a
+// number from misread weights.  (A NaN eps alone would not do: ReLU's fmax
+// turns the NaN activations into zeros.)
 __device__ __forceinline__ f32x4 packed_fragment(const f32x4* src4, int i, uint32_t tag) {
     f32x4 v = src4[i];
-    if (i == kB4 / 4 && __float_as_uint(src4[kTag / 4].x) != tag) v.w = __builtin_nanf("");
+    if (i == kB4 / 4 && __float_as_uint(src4[kTag / 4].x) != tag) {
+        const float q = __builtin_nanf("");
+        v = f32x4{q, q, q, q};
+    }
     return v;
 }
 
@@ -457,6 +461,9 @@ __device__ __forceinline__ void actor_sample(const float (&prob)[3], uint64_t en
         bits |= on ? (1u << k) : 0u;
         lp += bernoulli_logp(prob[k], on);
     }
+    // a NaN probability (packed_fragment's poison) makes the log-probability
+    // NaN too: the clamped Bernoulli log-probability alone would hide it
+    lp = fmaf(prob[0] + prob[1] + prob[2], 0.0f, lp);
 }
 
 }  // namespace mlp

@@ -149,6 +149,7 @@ EXPORTS = {
     "dd_step_bytes_per_env": (ctypes.c_int64, [_I, _I, _I]),
     "dd_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dd_abi_version": (ctypes.c_int, []),
+    "dd_build_info": (ctypes.c_char_p, []),
 }
 
 

@@ -107,3 +107,46 @@ def torch_mlp(sd: dict, device="cpu"):
     net = nn.Sequential(*layers)
     net.load_state_dict({kk: torch.as_tensor(v) for kk, v in sd.items()})
     return net.to(device).eval()
+
+
+def philox4x32_10_np(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 (Salmon et al., SC'11) over uint32 numpy arrays: the
+    vectorised twin of oracle.philox4x32_10 (tests pin the two together)."""
+    m0, m1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    w0, w1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+    mask = np.uint64(0xFFFFFFFF)
+    c = [np.asarray(v, dtype=np.uint32).copy() for v in (c0, c1, c2, c3)]
+    k0 = np.asarray(k0, dtype=np.uint32).copy()
+    k1 = np.asarray(k1, dtype=np.uint32).copy()
+    with np.errstate(over="ignore"):
+        for r in range(10):
+            p0 = m0 * c[0].astype(np.uint64)
+            p1 = m1 * c[2].astype(np.uint64)
+            hi0, lo0 = (p0 >> np.uint64(32)).astype(np.uint32), (p0 & mask).astype(np.uint32)
+            hi1, lo1 = (p1 >> np.uint64(32)).astype(np.uint32), (p1 & mask).astype(np.uint32)
+            c = [hi1 ^ c[1] ^ k0, lo1, hi0 ^ c[3] ^ k1, lo0]
+            if r < 9:
+                k0 = k0 + w0
+                k1 = k1 + w1
+    return c
+
+
+def philox_actions_np(seed: int, env0: int, n: int, step0: int, k: int) -> np.ndarray:
+    """include/dronestep.h DD_ACT_PHILOX for k steps from step0 and n lanes from
+    env id env0: step s's bitmask is nibble s & 31 of the Philox4x32-10 block
+    (key seed; counter env, s >> 5, with 0xA5A5A5A5 in the high word), low 3 bits."""
+    e = np.arange(env0, env0 + n, dtype=np.uint64)
+    out = np.zeros((k, n), dtype=np.uint8)
+    key0, key1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    blocks = {}
+    for t in range(k):
+        s = step0 + t
+        b = s >> 5
+        if b not in blocks:
+            blocks = {b: philox4x32_10_np(e & np.uint64(0xFFFFFFFF), e >> np.uint64(32),
+                                          np.full(n, b & 0xFFFFFFFF, np.uint32),
+                                          np.full(n, ((b >> 32) ^ 0xA5A5A5A5) & 0xFFFFFFFF, np.uint32),
+                                          np.full(n, key0, np.uint32), np.full(n, key1, np.uint32))}
+        word = blocks[b][(s >> 3) & 3]
+        out[t] = (word >> np.uint32(4 * (s & 7))) & np.uint32(7)
+    return out

@@ -33,3 +33,26 @@ def test_cpu_baseline_fields():
     r = b.cpu_baseline(0.3, 2, 0)
     assert set(r) >= {"value", "unit", "cores", "kind", "sample"}
     assert r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
+    assert set(r["legs"]) == {"python_objects", "c_scalar"}
+    assert r["value"] == r["legs"]["python_objects"]["value"]
+    assert r["legs"]["c_scalar"]["value"] > r["legs"]["python_objects"]["value"]  # C beats Python objects
+    assert r["host_cores"] == os.cpu_count() and r["affinity_cores"] >= 1 and r["cpu_model"]
+
+
+def test_pmc_traffic_only_for_the_measured_build(tmp_path):
+    # roofline.traffic must come from counters of the loaded build
+    from delivery_drone_amd import abi
+    b = _bench()
+    info = abi.lib().dd_build_info().decode()
+    assert info.startswith(f"abi={abi.DD_ABI_VERSION};step_isa=")
+    row = {"envs": 262144, "precision": "f32", "obs": True, "hbm_bytes_per_launch": 123}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"rows": [row]}))
+    v, note = b.pmc_traffic_row(262144, "f32", True, str(p))
+    assert v is None and "build_info" in note
+    p.write_text(json.dumps({"rows": [dict(row, build_info="abi=1;step_isa=0000000000000000")]}))
+    v, note = b.pmc_traffic_row(262144, "f32", True, str(p))
+    assert v is None and "step_isa" in note
+    p.write_text(json.dumps({"rows": [dict(row, build_info=info)]}))
+    assert b.pmc_traffic_row(262144, "f32", True, str(p))[0] == 123
+    assert b.pmc_traffic_row(4096, "f32", True, str(p))[0] is None

@@ -8,6 +8,10 @@ are 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 are the written bytes.  The two
 counters come from separate passes (FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2).
 
     python tools/pmc_summary.py OUT.json ENVS PRECISION OBS FETCH.csv WRITE.csv [...]
+
+Each row records the library's dd_build_info() (ABI version + step-kernel ISA
+hash) of the build the passes ran on — the in-tree libdronestep.so, which is
+what travels to the GPU box — so bench.py can refuse counters of another build.
 """
 import csv
 import json
@@ -22,8 +26,17 @@ def mean_counter(path, name):
     return sum(vals) / len(vals), len(vals)
 
 
+def build_info() -> str:
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "reinforcement-learning-101_amd"))
+    from delivery_drone_amd import abi
+    return abi.lib().dd_build_info().decode()
+
+
 def main():
     out = sys.argv[1]
+    info = build_info()
     args = sys.argv[2:]
     try:
         doc = json.load(open(out))
@@ -37,7 +50,7 @@ def main():
                "fetch_size_kib": round(fetch, 3), "write_size_kib": round(write, 3),
                "read_bytes_per_launch": int(2 * fetch * 1024), "write_bytes_per_launch": int(write * 1024),
                "hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024), "dispatches": [nf, nw],
-               "source": [fpath, wpath]}
+               "source": [fpath, wpath], "build_info": info}
         doc["rows"] = [r for r in doc["rows"] if not (r["envs"] == row["envs"] and r["precision"] == prec
                                                       and r["obs"] == row["obs"])] + [row]
     json.dump(doc, open(out, "w"), indent=1)
