@@ -302,30 +302,52 @@ def config2_point(seed, dev, n=4096):
             "rollout_steps_per_s": round(n * frames / (rms * 1e-3), 1)}
 
 
-def gather_point(env, n, world, backend, reps=5):
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def gather_point(obs, n, world, backend, reps=5):
     """BASELINE config 4's optional exchange: every rank's obs block [n, 15]
-    gathered to rank 0 (sharding.gather_obs: RCCL gather over xGMI), timed
-    outside the step loop.  Collective: every rank calls it."""
+    gathered to rank 0 (sharding.gather_obs: RCCL gather over xGMI with
+    backend nccl; gloo moves host copies), timed outside the step loop.
+    Collective: every rank calls it.  Rank 0 checks the gathered shape and
+    that its own block arrived unchanged (tests/test_bench_contract.py runs
+    this on gloo ranks)."""
     import torch
     import torch.distributed as dist
     from delivery_drone_amd.sharding import gather_obs
-    obs = env.obs if backend == "nccl" else env.obs.cpu()
+    dev = obs.device
+    obs = obs if backend == "nccl" else obs.cpu()
     gather_obs(obs, n * world)  # warm-up (communicator set-up)
-    torch.cuda.synchronize(env.device)
+    _sync(dev)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         out = gather_obs(obs, n * world)
-    torch.cuda.synchronize(env.device)
+    _sync(dev)
     dt = (time.perf_counter() - t0) / reps
-    t = torch.tensor([dt], dtype=torch.float64, device=env.device if backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t[0])
+    dt = reduce_max([dt], backend, dev)[0]
+    if dist.get_rank() == 0:
+        if tuple(out.shape) != (n * world, obs.shape[1]) or not torch.equal(out[:n], obs):
+            raise RuntimeError(f"gather_obs returned {tuple(out.shape)} / a changed rank-0 block")
     nbytes = n * world * 15 * 4
     del out
     return {"rows": n * world, "bytes_to_rank0": nbytes, "ms": round(dt * 1e3, 3),
             "GB_per_s": round(nbytes / dt / 1e9, 2), "backend": backend,
             "note": "timed outside the step loop; the step path has no collective"}
+
+
+def reduce_max(values, backend, dev):
+    """Element-wise max of `values` over all ranks (the bench's timing rule:
+    the slowest rank's wall and device time)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t]
 
 
 def gae_point(n, frames, dev):
@@ -695,11 +717,7 @@ def main():
         wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
 
-    stats = torch.tensor([wall, gpu_ms], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    wall, gpu_ms = float(stats[0]), float(stats[1])
+    wall, gpu_ms = reduce_max([wall, gpu_ms], args.dist_backend, dev)
 
     # sanity: the batch is alive and finite
     assert torch.isfinite(env.obs).all().item() and int(env.episode.max()) >= 1
@@ -709,7 +727,7 @@ def main():
     gp = None
     if world > 1:
         try:  # an optional extra: a failure here must not cost the step measurement
-            gp = gather_point(env, n, world, args.dist_backend)
+            gp = gather_point(env.obs, n, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
             gp = {"error": f"{type(e).__name__}: {e}"[:300]}
     c5 = c5a = g5 = c2 = nb = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None

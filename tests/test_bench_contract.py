@@ -56,3 +56,34 @@ def test_pmc_traffic_only_for_the_measured_build(tmp_path):
     p.write_text(json.dumps({"rows": [dict(row, build_info=info)]}))
     assert b.pmc_traffic_row(262144, "f32", True, str(p))[0] == 123
     assert b.pmc_traffic_row(4096, "f32", True, str(p))[0] is None
+
+
+def _gather_rank(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = _bench()
+    n = 1000
+    obs = torch.full((n, 15), float(rank)) + torch.arange(n, dtype=torch.float32)[:, None]
+    res = b.gather_point(obs, n, world, "gloo", reps=2)
+    mx = b.reduce_max([float(rank), -float(rank)], "gloo", obs.device)
+    if rank == 0:
+        with open(os.path.join(outdir, "gp.json"), "w") as f:
+            json.dump({"gp": res, "max": mx}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_multi_rank_helpers_on_gloo(tmp_path):
+    # bench.py's N>1 pieces (the obs gather point and the max-over-ranks timing
+    # reduction) on two gloo ranks; on the GPU node the same code runs on RCCL
+    import socket
+    import torch.multiprocessing as tmp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    tmp.spawn(_gather_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    d = json.load(open(tmp_path / "gp.json"))
+    assert d["gp"]["rows"] == 2000 and d["gp"]["bytes_to_rank0"] == 2000 * 60 and d["gp"]["backend"] == "gloo"
+    assert d["max"] == [1.0, 0.0]

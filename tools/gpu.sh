@@ -15,6 +15,7 @@
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the step kernel at 262,144 and 16.8M drones
 #   sq         SQ instruction counters of the step / rollout kernels (tools/pmc_sq.sh)
 #   lab        tools/kernel_lab.py (VARIANTS, ENVS, LABARGS)
+#   mr         tools/multirank_check.py on 2 gloo ranks sharing GPU 0 (torchrun), output in <tag>/mr/
 #   py:<file>  python <file> (LABARGS passed through), output in <tag>/<file stem>.log
 set -o pipefail
 TAG=${1:?tag}
@@ -60,6 +61,10 @@ run_step() {
     lab)
         timeout -k 10 600 python tools/kernel_lab.py --variants ${VARIANTS:-base} --envs ${ENVS:-262144,1048576,16777216} \
             ${LABARGS} > $OUT/lab.jsonl 2> $OUT/lab.err; local rc=$?; cat $OUT/lab.jsonl; tail -5 $OUT/lab.err; return $rc ;;
+    mr)
+        timeout -k 10 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+            --master-port 29517 tools/multirank_check.py --backend gloo --out $OUT/mr > $OUT/mr.log 2>&1; local rc=$?
+        tail -3 $OUT/mr.log; return $rc ;;
     py:*)
         local f=${1#py:}; local stem=$(basename ${f%.py})
         timeout -k 10 ${PYTIMEOUT:-600} python -u $f ${LABARGS} > $OUT/$stem.log 2>&1; local rc=$?
