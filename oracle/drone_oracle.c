@@ -354,6 +354,30 @@ int ora_step(const DDConfig *c, const DDState *st, const uint8_t *actions, void 
     return ora_step_shaped(c, st, actions, reward, done, obs, obs64, NULL, NULL, NULL, 0, n);
 }
 
+/* Threshold probing (tests/threshold_states.py): the post-update quantities
+ * the reward cascade compares, for a live lane stepped with `actions` — x', y',
+ * speed', angle', the bottom centre (bx', by') and vx', vy' — as q[i*8 + 0..7].  The
+ * lanes' state is not modified. */
+int ora_probe(const DDConfig *c, const DDState *st, const uint8_t *actions, double *q, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) {
+        OraLane s;
+        load_lane(st, i, &s);
+        s.status = 0;
+        ora_frame(c, actions[i], &s);
+        double ox, oy;
+        rotate_y(c->drone_half_height, s.angle, &ox, &oy);
+        q[i * 8 + 0] = s.x;
+        q[i * 8 + 1] = s.y;
+        q[i * 8 + 2] = speed_of(&s);
+        q[i * 8 + 3] = s.angle;
+        q[i * 8 + 4] = s.x + ox;
+        q[i * 8 + 5] = s.y + oy;
+        q[i * 8 + 6] = s.vx;
+        q[i * 8 + 7] = s.vy;
+    }
+    return 0;
+}
+
 int ora_reset(const DDConfig *c, const DDState *st, const uint8_t *mask, float *obs, double *obs64, int64_t n) {
     for (int64_t i = 0; i < n; ++i) {
         if (mask && !mask[i]) continue;

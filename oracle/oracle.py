@@ -53,6 +53,7 @@ def lib() -> ctypes.CDLL:
                 h.ora_reset.argtypes = [cfgp, stp, P, P, P, ctypes.c_int64]
                 h.ora_write_obs.argtypes = [cfgp, stp, P, P, ctypes.c_int64]
                 h.ora_get_info.argtypes = [cfgp, stp, P, P, ctypes.c_int64]
+                h.ora_probe.argtypes = [cfgp, stp, P, P, ctypes.c_int64]
                 h.ora_philox4x32_10.argtypes = [P, P, P]
                 h.ora_philox4x32_10.restype = None
                 h.ora_bench.argtypes = [cfgp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
@@ -153,6 +154,14 @@ class OracleEnv:
         st = self._state()
         lib().ora_write_obs(ctypes.byref(self._cfg), ctypes.byref(st), _p(obs), _p(obs64), self.n)
         return obs, obs64
+
+    def probe(self, actions):
+        """Post-update (x, y, speed, angle, bottom x, bottom y, vx, vy) of every
+        lane stepped with `actions`, as [n, 8] float64; the state is unchanged."""
+        a = bitmask(actions)
+        q = np.zeros((self.n, 8), dtype=np.float64)
+        lib().ora_probe(ctypes.byref(self._cfg), ctypes.byref(self._state()), _p(a), _p(q), self.n)
+        return q
 
     def get_info(self):
         d = np.zeros(self.n)

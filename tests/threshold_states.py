@@ -1,0 +1,147 @@
+"""States whose post-update quantities sit within a few ulps of the reward
+cascade's predicate boundaries (game_engine.py:218-279, drone.py:130-153),
+for the flag parity sweep (tests/test_gpu_thresholds.py).
+
+Families (each a share of the batch), the boundary and the variable moved:
+
+  crash_y     y' = 550 (ground_level)                 y
+  oob         x' = -50 / 850, y' = -50                x / y
+  speed       speed' = 3 on the pad (landing test)     vx, vy (scaled)
+  angle       |angle'| = 20 on the pad                 angle
+  pad_x       bottom-centre x' = px -/+ 50, slow, upright   x
+  pad_y       bottom-centre y' = py -/+ 10, slow, upright   y
+  fuel        fuel' = 0 (fuel 0-3 with every action)   (exact)
+
+Targets are boundary + k ulps, k uniform in [-4, 4], in the storage width's
+ulps (double for "f64", float32 for "f32" — a float32 state cannot put a
+double sum within a few double ulps of a boundary).  The variable is moved
+by Newton steps on the oracle's own post-update quantities (OracleEnv.probe,
+libm trig and pow as the reference), so the states are near the boundaries
+the reference sees.  Main-engine firing is random, so the thrust vector's
+sin/cos feeds every family but fuel.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+FAMILIES = ("crash_y", "oob", "speed", "angle", "pad_x", "pad_y", "fuel")
+Q_X, Q_Y, Q_SPEED, Q_ANGLE, Q_BX, Q_BY, Q_VX, Q_VY = range(8)
+
+
+def _ulp(v, precision):
+    v = np.abs(np.asarray(v, np.float64))
+    if precision == "f64":
+        return np.spacing(v)
+    return np.spacing(v.astype(np.float32)).astype(np.float64)
+
+
+def _base(rng, n):
+    st = dict(
+        x=rng.uniform(-40, 840, n), y=rng.uniform(-40, 640, n), vx=rng.uniform(-8, 8, n),
+        vy=rng.uniform(-8, 12, n), angle=rng.uniform(-180, 180, n), omega=rng.uniform(-6, 6, n),
+        fuel=rng.integers(4, 1001, n).astype(np.float64), px=rng.integers(100, 700, n).astype(np.float64),
+        py=rng.integers(100, 540, n).astype(np.float64), total_reward=np.zeros(n),
+        status=np.zeros(n, np.uint8), steps=rng.integers(0, 500, n).astype(np.int32),
+        episode=np.ones(n, np.int32))
+    acts = rng.integers(0, 8, n).astype(np.uint8)
+    return st, acts
+
+
+def _near_pad(rng, st, idx):
+    """Slow, upright drones hovering over their pad (the landing branch)."""
+    m = idx.size
+    ang = rng.uniform(-15, 15, m)
+    st["angle"][idx] = ang
+    st["omega"][idx] = rng.uniform(-0.5, 0.5, m)
+    st["vx"][idx] = rng.uniform(-1.5, 1.5, m)
+    st["vy"][idx] = rng.uniform(-2.0, 1.0, m)
+    st["x"][idx] = st["px"][idx] + rng.uniform(-45, 45, m)
+    st["y"][idx] = st["py"][idx] - 10 + rng.uniform(-8, 8, m)
+
+
+def generate(n: int, precision: str, seed: int = 0, iters: int = 6):
+    """(state dict, actions u8 [n], family index [n], target [n], which q column
+    [n]) with the targeted quantity within ~4 storage ulps of its boundary."""
+    from oracle import oracle as ora
+    from delivery_drone_amd import EnvConfig
+
+    rng = np.random.default_rng(seed)
+    st, acts = _base(rng, n)
+    fam = rng.integers(0, len(FAMILIES), n)
+    col = np.zeros(n, np.int64)
+    bound = np.zeros(n)
+    var = np.empty(n, dtype=object)
+    for f, name in enumerate(FAMILIES):
+        idx = np.flatnonzero(fam == f)
+        m = idx.size
+        if name == "crash_y":
+            col[idx], bound[idx], var[idx] = Q_Y, 550.0, "y"
+            st["px"][idx] = rng.integers(100, 700, m)  # pads anywhere; some under the drone
+            st["py"][idx] = rng.integers(520, 560, m)
+            st["x"][idx] = st["px"][idx] + rng.uniform(-80, 80, m)
+            st["vy"][idx] = rng.uniform(-1, 6, m)
+            sel = rng.random(m) < 0.5  # half slow and upright: the on-pad crash tests
+            _near_pad(rng, st, idx[sel])
+            st["py"][idx[sel]] = rng.integers(545, 556, int(sel.sum()))
+        elif name == "oob":
+            side = rng.integers(0, 3, m)
+            col[idx] = np.where(side < 2, Q_X, Q_Y)
+            bound[idx] = np.choose(side, [-50.0, 850.0, -50.0])
+            var[idx] = np.where(side < 2, "x", "y")
+        elif name == "speed":
+            _near_pad(rng, st, idx)
+            col[idx], bound[idx], var[idx] = Q_SPEED, 3.0, "speed"
+            st["vx"][idx] = rng.uniform(-3, 3, m)
+            st["vy"][idx] = rng.uniform(-3, 3, m)
+        elif name == "angle":
+            _near_pad(rng, st, idx)
+            sign = np.where(rng.random(m) < 0.5, -1.0, 1.0)
+            col[idx], bound[idx], var[idx] = Q_ANGLE, 20.0 * sign, "angle"
+            st["angle"][idx] = 20.0 * sign
+        elif name == "pad_x":
+            _near_pad(rng, st, idx)
+            sign = np.where(rng.random(m) < 0.5, -1.0, 1.0)
+            col[idx], bound[idx], var[idx] = Q_BX, st["px"][idx] + 50.0 * sign, "x"
+        elif name == "pad_y":
+            _near_pad(rng, st, idx)
+            sign = np.where(rng.random(m) < 0.5, -1.0, 1.0)
+            col[idx], bound[idx], var[idx] = Q_BY, st["py"][idx] + 10.0 * sign, "y"
+        else:  # fuel: exact arithmetic, every action with 0-3 units left
+            st["fuel"][idx] = rng.integers(0, 4, m)
+            col[idx], bound[idx], var[idx] = Q_Y, np.nan, ""
+    k = rng.integers(-4, 5, n)
+    target = bound + k * _ulp(bound, precision)
+    dt = np.float64 if precision == "f64" else np.float32
+    cfg = EnvConfig()
+
+    def quantize():
+        for f in ("x", "y", "vx", "vy", "angle", "omega", "fuel"):
+            st[f] = st[f].astype(dt).astype(np.float64)
+
+    quantize()
+    moved = var != ""
+    for _ in range(iters):
+        o = ora.OracleEnv(n, precision="f64", config=cfg)
+        o.load_state_dict(st)
+        q = o.probe(acts)
+        cur = q[np.arange(n), col]
+        err = np.where(moved, target - cur, 0.0)
+        for v in ("x", "y", "angle"):
+            sel = var == v
+            st[v][sel] = st[v][sel] + err[sel]
+        # speed' = |0.99 (v + thrust + gravity)|: a Newton step on the larger
+        # post-update component (d speed' / d v = 0.99 v' / speed')
+        sel = (var == "speed") & (cur > 0)
+        vxp, vyp = q[:, Q_VX], q[:, Q_VY]
+        use_x = np.abs(vxp) >= np.abs(vyp)
+        comp = np.where(use_x, vxp, vyp)
+        step = np.where(sel & (comp != 0), err * cur / (0.99 * np.where(comp != 0, comp, 1.0)), 0.0)
+        st["vx"] = np.where(sel & use_x, st["vx"] + step, st["vx"])
+        st["vy"] = np.where(sel & ~use_x, st["vy"] + step, st["vy"])
+        quantize()
+    o = ora.OracleEnv(n, precision="f64", config=cfg)
+    o.load_state_dict(st)
+    q = o.probe(acts)
+    cur = q[np.arange(n), col]
+    dist_ulps = np.where(moved, np.abs(cur - bound) / _ulp(bound, precision), 0.0)
+    return st, acts, fam, dist_ulps
