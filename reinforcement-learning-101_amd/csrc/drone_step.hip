@@ -261,10 +261,12 @@ __device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, u
 
 // Everything after the loads for one lane: the frame (or sticky done / auto
 // reset), the state and output stores, the observation row into `orow`
-// (LDS).  Returns whether the lane's episode ended in this call.
-template <typename T, bool kRef, bool kShaped>
+// (LDS).  Returns whether the lane's episode ended in this call.  The fast
+// frame (kExact false) may report the lane risky (frame.h): then nothing is
+// stored, and the kernel calls finish_lane again with kExact.
+template <typename T, bool kRef, bool kShaped, bool kExact = false>
 __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, uint32_t i, const Raw<T>& r,
-                                            float* orow) {
+                                            float* orow, bool* risky = nullptr) {
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     Lane s;
@@ -298,11 +300,18 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
         reward = s.x;
         s.status |= (s.y > 550.0) ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
 #else
-        reward = frame<kRef, false>(k, sw, r.act, s);
+        bool rk = false;
+        reward = frame<kRef, false, kExact>(k, sw, r.act, s, &rk);
+        if constexpr (!kExact) {
+            if (__builtin_expect(rk, 0)) {  // the exact pass redoes this lane: store nothing now
+                *risky = true;
+                return false;
+            }
+        }
 #endif
         if constexpr (kShaped) {
             double v[13];
-            observe_values(k, s, v);
+            observe_values<false, true>(k, s, v);  // the notebook reward's doubles: exact quotients
             double* slot = p.shaped_hist + (s.steps & 1) * p.hist_stride;  // two frames back
             shaped = notebook_reward(v, s.status, at(slot, i));
             at(slot, i) = v[9];
@@ -312,7 +321,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
                 shaped_done = true;
                 s.status |= DD_ST_DONE;  // the episode ends here (TimeLimit)
             }
-            if (p.obs) write_obs_row(v, s.status, orow);
+            if (p.obs) observe(k, s, orow);  // rows as every other path writes them
         }
         ended = (s.status & DD_ST_DONE) != 0;
     }
@@ -389,7 +398,11 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     DD_TL(1);
 #endif
-    const bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM);
+    bool risky = false;
+    bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM, &risky);
+    if (__builtin_expect(__ballot(risky) != 0, 0)) {  // the rare exact pass (frame.h): glibc's sin, cos and pow
+        if (risky) ended = finish_lane<T, kRef, kShaped, true>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM);
+    }
     DD_TL(2);
     if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
         const uint64_t m = __ballot(ended);
@@ -619,7 +632,7 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
             // next-step reset, fixed up after the frame: every lane runs the
             // frame (a done lane's result is discarded), and a wave with a lane
             // to re-spawn takes the one branch
-            reward = frame<kRef, true>(k, sw, act, s);
+            reward = frame_checked<kRef, true>(k, sw, act, s);
             if (__ballot(was_done)) {
                 if (was_done) {
                     spawn(sw, k.c.max_fuel, env, s);
@@ -630,13 +643,13 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
             measure(s);
             reward = 0.0;
         } else {
-            reward = frame<kRef, true>(k, sw, act, s);
+            reward = frame_checked<kRef, true>(k, sw, act, s);
         }
         if constexpr (kShaped) {
             // dd_step's notebook path (finish_lane) with the history in h0 / h1:
             // slot steps & 1 holds the distance two frames back
             double v[13];
-            observe_values<kGuard>(k, s, v);
+            observe_values<kGuard, true>(k, s, v);  // the notebook reward's doubles: exact quotients
             double shaped = 0.0;
             bool shaped_done;
             if (kAuto && was_done) {  // re-spawned: the history restarts (prev_state None)
@@ -663,7 +676,7 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
                 put_out(reinterpret_cast<T*>(p.engine_reward + f * p.reward_stride), i, (T)reward);
                 put_out(p.engine_done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
             }
-            if constexpr (kObs) write_obs_row(v, s.status, tile[kHeld ? (f & 1) : 0] + roff);
+            if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
         } else {
             put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
             put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));

@@ -16,20 +16,53 @@
 #include "philox.h"
 #include "trig.h"
 
+// The reference's sin, cos and squares, bit for bit: libm_ref.h restates
+// glibc's (the reference calls np.sin / np.cos and `v ** 2` = glibc pow), with
+// their tables (tools/gen_libm_tables.py, from this image's libm) in device
+// memory, for the rare frames near a predicate boundary (frame).
+#include "libm_tables.h"
+__device__ const double dd_libm_pow_tab[384] = DD_LIBM_POW_TAB;
+__device__ const uint64_t dd_libm_exp_tab[256] = DD_LIBM_EXP_TAB;
+__device__ const double dd_libm_sincos_tab[440] = DD_LIBM_SINCOS_TAB;
+#define DD_LIBM_FN __device__ __forceinline__
+#define DD_LIBM_OPAQUE
+#ifdef DD_EXP_LIBM_CALLS
+#define DD_LIBM_ENTRY __device__ __noinline__
+#define DD_LIBM_SINCOS_FN __device__ __noinline__
+#else
+#define DD_LIBM_ENTRY __device__ __forceinline__
+#endif
+#include "libm_ref.h"
+#undef DD_LIBM_FN
+#undef DD_LIBM_ENTRY
+#undef DD_LIBM_SINCOS_FN
+#undef DD_LIBM_OPAQUE
+
 namespace dd {
 
 // numpy's deg2rad: x * (NPY_PI / 180.0)   (physics.py:16, np.radians)
 constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
 
 // sin and cos of an angle in degrees, as rotate_point computes them
-// (physics.py:16-18).  DD_TRIG_OCML selects the ROCm device library's
-// general-argument sincos instead of trig.h's (timing experiments).
+// (physics.py:16-18: np.radians, then np.cos and np.sin).  Fast: trig.h's
+// (within an ulp of glibc's); kExact: glibc's, bit for bit (libm_ref.h), for
+// the rare frames where an ulp could flip a flag (frame).  Lab switches for
+// the fast one: DD_TRIG_GLIBC (glibc's everywhere: +9 % step, +26 % rollout
+// with the table in global memory), DD_TRIG_OCML (the ROCm device
+// library's), DD_EXP_FAKE_TRIG (timing only).
+template <bool kExact = false>
 __device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
+    if constexpr (kExact) {
+        libm::sincos(deg * kDeg2Rad, s, c);
+        return;
+    }
 #if defined(DD_EXP_FAKE_TRIG)  // timing-only sensitivity: what the trig costs
     *s = deg * 1e-3;
     *c = 1.0 - fabs(*s);
 #elif defined(DD_TRIG_OCML)
     ::sincos(deg * kDeg2Rad, s, c);
+#elif defined(DD_TRIG_GLIBC)
+    libm::sincos(deg * kDeg2Rad, s, c);
 #else
     trig::sincos(deg * kDeg2Rad, s, c);
 #endif
@@ -152,16 +185,23 @@ struct Lane {
 };
 
 // Drone.get_speed (drone.py:139-145) and physics.distance (physics.py:42-44)
-// of the current state; both the reward and get_state use them.
-__device__ __forceinline__ void measure(Lane& s) {
+// of the current state; both the reward and get_state use them.  Returns the
+// speed's sum of squares.  The reference squares with `v ** 2`, glibc pow,
+// which differs from v*v by an ulp on ~0.09 % of inputs: speed and distance
+// may differ from the reference's by an ulp (the observation and the shaping
+// reward's tolerance); the one flag they decide, slow, is made exact in
+// frame().
+__device__ __forceinline__ double measure(Lane& s) {
     const double dx = s.px - s.x, dy = s.py - s.y;
+    const double ss = s.vx * s.vx + s.vy * s.vy;
 #ifdef DD_EXP_FAKE_SQRT  // timing-only sensitivity: what the two square roots cost
-    s.speed = (s.vx * s.vx + s.vy * s.vy) * 0.25;
+    s.speed = ss * 0.25;
     s.dist = (dx * dx + dy * dy) * 0.001;
 #else
-    s.speed = sqrt(s.vx * s.vx + s.vy * s.vy);
+    s.speed = sqrt(ss);
     s.dist = sqrt(dx * dx + dy * dy);
 #endif
+    return ss;
 }
 
 // DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
@@ -227,16 +267,16 @@ __device__ __forceinline__ double wrap_angle(double a) {
 // The step kernel (four waves per SIMD) keeps the branches: selects cost it
 // VALU slots the other waves would use.  Only the bottom-centre test near
 // the pad (rare) branches in both.
-template <bool kRef, bool kFlat>
-__device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
+template <bool kRef, bool kFlat, bool kExact = false>
+__device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s, bool* risky_out) {
     const DDConfig& c = k.c;
 
     // apply_thrust: each thruster gated on fuel > 0 at that moment, in order
     const double ty = -c.main_thrust_power;
+    const bool main_on = (act & 1u) && s.fuel > 0.0;
     if constexpr (kFlat) {
-        const bool main_on = (act & 1u) && s.fuel > 0.0;
         double sa, ca;
-        sincos_deg(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
+        sincos_deg<kExact>(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
         s.vx = main_on ? s.vx + (0.0 * ca - ty * sa) : s.vx;
         s.vy = main_on ? s.vy + (0.0 * sa + ty * ca) : s.vy;
         s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
@@ -247,9 +287,9 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         s.omega = right_on ? s.omega + c.side_thrust_power : s.omega;
         s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
     } else {
-        if ((act & 1u) && s.fuel > 0.0) {
+        if (main_on) {
             double sa, ca;
-            sincos_deg(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)
+            sincos_deg<kExact>(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)
             s.vx += 0.0 * ca - ty * sa;
             s.vy += 0.0 * sa + ty * ca;
             s.fuel -= c.fuel_main;
@@ -281,35 +321,86 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         else if (s.px >= c.platform_max_x) { s.px = c.platform_max_x; s.status |= DD_ST_PLAT_LEFT; }
     }
 
-    measure(s);  // speed (get_speed) and distance (physics.distance), shared with get_state
-    const bool slow = !(s.speed > c.max_landing_velocity);
-    const bool upright = fabs(s.angle) <= c.max_landing_angle;
+    // Exactness.  The cascade's predicates are the reference's bit for bit
+    // when their inputs are: every operation here is the reference's, but the
+    // fast sincos (trig.h) may differ from glibc's by an ulp, and the speed's
+    // squares (v*v here, glibc pow there) too.  Those can only flip a flag
+    // when a compared quantity lies within a few ulps of its boundary, so the
+    // fast frame reports such a lane in *risky_out and the kernel runs its
+    // frame again with kExact (glibc's sin, cos and pow: libm_ref.h) out of
+    // its hot loop:
+    // * x' or y' (thrust-dependent) near an out-of-bounds or ground boundary:
+    //   under kRef x', y' rounded to float equal to -50 / 850 / -50 / 550
+    //   (within half a float ulp, >= 1.9e-6; four f32 compares on the
+    //   conversions the f32 store makes anyway);
+    // * on the landing test's lanes (upright, within reach of the pad): the
+    //   speed or the bottom centre within 2^-20 of its limit / a pad edge.
+    // y' = 650 never decides a flag (past 550 the drone has crashed or landed
+    // first); fuel, spin and angle involve no transcendental.
+    const auto close = [](double q, double b) { return fabs(q - b) <= 0x1p-20 * (1.0 + fabs(b)); };
+    bool risky = false;
+    if constexpr (!kExact) {
+        if constexpr (kRef) {
+            constexpr DDConfig r = reference_config();
+            static_assert(-r.oob_margin == -50 && r.world_width + r.oob_margin == 850 && r.ground_level == 550,
+                          "float boundary constants");
+            const float xf = (float)s.x, yf = (float)s.y;
+            const bool q0 = xf == -50.0f, q1 = xf == 850.0f, q2 = yf == -50.0f, q3 = yf == 550.0f;
+            risky = q0 | q1 | q2 | q3;
+        } else {
+            const bool q0 = close(s.y, c.ground_level), q1 = close(s.x, -c.oob_margin),
+                       q2 = close(s.x, c.world_width + c.oob_margin), q3 = close(s.y, -c.oob_margin);
+            risky = q0 | q1 | q2 | q3;
+        }
+    }
 
-    // get_bottom_center: rotate_point(0, height / 2, angle) on the updated
-    // angle.  It only matters through on_pad, and the bottom centre lies
-    // within |half_height| (+ rounding) of (x, y), so the rotation (the
-    // frame's second sincos) runs only for slow, upright drones within that
-    // reach of the pad; every other lane has on_pad = false exactly as the
-    // reference's comparisons would give (NaN fails both tests alike).
-    bool on_pad = false;
+    const double ss = measure(s);  // speed (get_speed), distance (physics.distance), shared with get_state
+    const bool upright = fabs(s.angle) <= c.max_landing_angle;
+    bool on_pad = false;  // _check_landing: bottom centre on the platform, slow and upright
     const double rx = c.platform_half_width + fabs(c.drone_half_height);
     const double ry = c.platform_half_height + fabs(c.drone_half_height);
     const double slack = 1.0 + 1e-9 * (fabs(s.x) + fabs(s.y) + fabs(s.px) + fabs(s.py) + rx + ry);
-    if (slow && upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack) {
-        double sb, cb;
-        sincos_deg(s.angle, &sb, &cb);
-        const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
-        const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
-        on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
-                 (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
+    if (upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack) {
+        // (lanes out of this reach of the pad: on_pad = false exactly as the
+        // reference's comparisons give, the bottom centre lying within
+        // |half_height| (+ rounding) of (x, y); NaN fails both tests alike)
+        const bool edge = kRef ? fabs(ss - 9.0) <= 0x1p-20 : close(s.speed, c.max_landing_velocity);
+        bool slow = !(s.speed > c.max_landing_velocity);
+        if constexpr (kExact) {
+            if (edge) {  // the reference's speed: sqrt(pow(vx, 2) + pow(vy, 2))
+                double sq = 0.0, v = s.vx;
+#pragma unroll 1
+                for (int q = 0; q < 2; ++q) {
+                    sq += libm::pow2(v);
+                    v = s.vy;
+                }
+                slow = !(sqrt(sq) > c.max_landing_velocity);
+            }
+        } else {
+            risky |= edge;
+        }
+        if (slow) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
+            double sb, cb;
+            sincos_deg<kExact>(s.angle, &sb, &cb);
+            const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
+            const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
+            on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
+                     (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
+            if constexpr (!kExact) {
+                const bool e0 = close(bx, s.px - c.platform_half_width), e1 = close(bx, s.px + c.platform_half_width),
+                           e2 = close(by, s.py - c.platform_half_height), e3 = close(by, s.py + c.platform_half_height);
+                risky |= e0 | e1 | e2 | e3;
+            }
+        }
     }
+    if constexpr (!kExact) *risky_out = risky;
 
     // _calculate_reward's cascade, evaluated branch-free: every predicate is
     // formed, then the first that holds picks the term.  (The nested
     // else-if form miscompiled on ROCm 7.2 / gfx950: the divergent-branch phi
     // register of the out-of-bounds term was reused as a temporary, giving
     // 649.9 instead of -50.1; tests/test_gpu_parity.py pins every branch.)
-    const bool landing = on_pad & slow & upright;                         // _check_landing
+    const bool landing = on_pad;  // _check_landing: on the pad, slow (the reference's speed) and upright
     const bool crash = s.y > c.ground_level;                              // _check_crash, landing ruled out
     const bool no_fuel = s.fuel <= 0.0;
     const bool oob = (s.x < -c.oob_margin) | (s.x > c.world_width + c.oob_margin) |
@@ -339,18 +430,41 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     return reward;
 }
 
-// DroneGame.get_state (game_engine.py:140-177) in state_to_array order, as the
-// reference's doubles (columns 0-12; 13/14 are the landed / crashed flags);
-// measure() has run on `s`.
-template <bool kGuard = false>
+
+
+// A frame for kernels that keep the lane's state in registers (the rollout
+// loops): the fast frame, and for a lane it reports risky the frame again
+// from the kept state with glibc's functions (a wave-uniform rare branch).
+template <bool kRef, bool kFlat>
+__device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
+    const Lane s0 = s;
+    bool risky = false;
+    double reward = frame<kRef, kFlat>(k, sw, act, s, &risky);
+    if (__builtin_expect(__ballot(risky) != 0, 0)) {
+        if (risky) {
+            s = s0;
+            reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
+        }
+    }
+    return reward;
+}
+
+// DroneGame.get_state (game_engine.py:140-177) in state_to_array order, as
+// doubles (columns 0-12; 13/14 are the landed / crashed flags); measure() has
+// run on `s`.  kExactDiv: the reference's quotients bit for bit (x / d by
+// trig::div_exact, 3 ops) — the notebook reward consumes these doubles.
+// Otherwise x * RN(1/d), one op per column: within one double ulp of the
+// quotient, and identical after the float32 rounding of an observation row
+// except when the quotient lies within ~1e-16 relative of a float32 rounding
+// boundary (0 of 2e7 random values per divisor, 0 of the integer spawn
+// positions: tools/obs_mul_check.py) — inside the rows' 1-ulp contract.
+// Saves 26 of the rollout frame's ~360 VALU ops.
+template <bool kGuard = false, bool kExactDiv = false>
 __device__ __forceinline__ void observe_values(const Consts& k, const Lane& s, double v[13]) {
     const DDConfig& c = k.c;
     const double dx = s.px - s.x, dy = s.py - s.y;
-#ifdef DD_OBS_MUL  // experiment: x * RN(1/d), one op per column instead of three
-#define DD_Q(x, d, inv) ((x) * (inv))
-#else
-#define DD_Q(x, d, inv) (kGuard ? trig::div_exact_guarded((x), (d), (inv)) : trig::div_exact((x), (d), (inv)))
-#endif
+#define DD_Q(x, d, inv) \
+    (!kExactDiv ? (x) * (inv) : kGuard ? trig::div_exact_guarded((x), (d), (inv)) : trig::div_exact((x), (d), (inv)))
     v[0] = DD_Q(s.x, c.world_width, k.inv_w);
     v[1] = DD_Q(s.y, c.world_height, k.inv_h);
     v[2] = DD_Q(s.vx, c.vel_scale, k.inv_vel);

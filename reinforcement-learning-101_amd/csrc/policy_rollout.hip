@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
         const bool was_done = (s.status & DD_ST_DONE) != 0;
         double reward;
         if (sw.auto_reset) {  // next-step reset: the frame's result is discarded for a done lane
-            reward = frame<kRef, true>(k, sw, act, s);
+            reward = frame_checked<kRef, true>(k, sw, act, s);
             if (__ballot(was_done)) {
                 if (was_done) {
                     spawn(sw, k.c.max_fuel, env, s);
@@ -188,13 +188,13 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
             measure(s);
             reward = 0.0;
         } else {
-            reward = frame<kRef, true>(k, sw, act, s);
+            reward = frame_checked<kRef, true>(k, sw, act, s);
         }
         T* rew = reinterpret_cast<T*>(p.reward) + fo + d;
         uint8_t* dn = p.done + fo + d;
         if (shaped) {  // dd_step's notebook path with the history in h0 / h1
             double v[13];
-            observe_values<kGuard>(k, s, v);
+            observe_values<kGuard, true>(k, s, v);  // the notebook reward's doubles: exact quotients
             double sr = 0.0;
             bool sd;
             if (sw.auto_reset && was_done) {  // re-spawned: prev_state None

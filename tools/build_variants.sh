@@ -5,14 +5,14 @@ set -e
 cd "$(dirname "$0")/../reinforcement-learning-101_amd"
 OUT=delivery_drone_amd/_native/lab
 mkdir -p $OUT
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I../include"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I../include -Ibuild"
 build() { /opt/rocm/bin/hipcc $FLAGS "${@:2}" -o $OUT/lib_$1.so csrc/drone_step.hip csrc/policy_mlp.hip csrc/policy_rollout.hip csrc/render.hip & }
 # "prev": the committed source at $PREV_REV (default HEAD), for before/after runs
 if [ -n "${PREV_REV:-HEAD}" ] && git -C .. rev-parse -q --verify "${PREV_REV:-HEAD}" > /dev/null 2>&1; then
   mkdir -p /tmp/dd_prev
   git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/drone_step.hip" > /tmp/dd_prev/drone_step.hip
   PREV_SRCS=/tmp/dd_prev/drone_step.hip
-  for f in trig.h philox.h frame.h mlp_core.h policy_mlp.hip policy_rollout.hip render.hip font_atlas.h; do
+  for f in trig.h philox.h frame.h libm_ref.h mlp_core.h policy_mlp.hip policy_rollout.hip render.hip font_atlas.h; do
     git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/$f" > /tmp/dd_prev/$f 2>/dev/null || rm -f /tmp/dd_prev/$f
   done
   [ -f /tmp/dd_prev/policy_mlp.hip ] && PREV_SRCS="$PREV_SRCS /tmp/dd_prev/policy_mlp.hip"
@@ -28,7 +28,6 @@ for v in ${VARIANTS:-base}; do
     nofma) build nofma -DDD_TRIG_NO_FMA ;;
     plainout) build plainout -DDD_ST_OUT=0 ;;
     nomath) build nomath -DDD_EXP_NOMATH ;;
-    obsmul) build obsmul -DDD_OBS_MUL ;;
     mlpw4) build mlpw4 -DDD_MLP_WAVES=4 ;;
     mlpw12) build mlpw12 -DDD_MLP_WAVES=12 ;;
     empty) build empty -DDD_EXP_EMPTY ;;
@@ -56,6 +55,8 @@ for v in ${VARIANTS:-base}; do
     tlwtall) build tlwtall -DDD_EXP_TIMELINE -DDD_ST_STATE=1 -DDD_ST_OUT=1 -DDD_ST_OBS=1 ;;
     ieeerstd) build ieeerstd -DDD_MLP_IEEE_RSTD ;;
     pad*) build $v -DDD_EXP_PAD_VALU=${v#pad} ;;
+    glibctrig) build glibctrig -DDD_TRIG_GLIBC ;;
+    noexact) build noexact -DDD_EXP_NO_EXACT ;;
     mpad*) build $v -DDD_MLP_PAD=${v#mpad} ;;
     log1p) build log1p -DDD_MLP_LOG1P ;;
     serial) build serial -DDD_MLP_SERIAL ;;

@@ -7,7 +7,7 @@
 # failure ends the session (a fault, abort or time-out starts nothing more on
 # the GPU).  Output goes to gpurun_out/<tag>/.
 #
-#   tests      pytest -m gpu (PYTEST_ARGS adds options, e.g. -k)
+#   tests      pytest -m gpu (PYTEST_K: a -k expression)
 #   smoke      __graft_entry__.smoke()
 #   bench20    the driver's line: bench.py --gpus 1 --steps 20 --warmup 5
 #   bench      bench.py with its defaults (every extra point)
@@ -27,8 +27,8 @@ export TMPDIR=/tmp
 run_step() {
     case "$1" in
     tests)
-        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} \
-            > $OUT/pytest_gpu.log 2>&1; local rc=$?; tail -2 $OUT/pytest_gpu.log; return $rc ;;
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+            ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1; local rc=$?; tail -2 $OUT/pytest_gpu.log; return $rc ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; local rc=$?
         tail -1 $OUT/smoke.log; return $rc ;;

@@ -34,6 +34,8 @@ def main():
     p.add_argument("--rounds", type=int, default=9)
     p.add_argument("--precision", default="f32")
     p.add_argument("--no-obs", action="store_true")
+    p.add_argument("--separate", dest="shared", action="store_false",
+                   help="one env per variant (default: every variant steps the same buffers)")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     libs = {v: abi.load(os.path.join(LAB, f"lib_{v}.so")) for v in args.variants.split(",")}
@@ -43,9 +45,15 @@ def main():
         rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
         stream = torch.cuda.Stream(dev)
         runs = {}
+        shared = None
         for name, lib in libs.items():
-            env = VecDroneEnv(n, device=dev, config=cfg, precision=args.precision, library=lib)
-            env.reset()
+            if shared is None or not args.shared:
+                env = VecDroneEnv(n, device=dev, config=cfg, precision=args.precision, library=lib)
+                env.reset()
+                shared = env
+            else:  # the same buffers, another build: physical placement out of the A/B
+                env = shared
+            env._lib = lib
             with torch.cuda.stream(stream):
                 for k in range(3):
                     env.step(rows[k], write_obs=not args.no_obs)

@@ -31,9 +31,13 @@ def main():
         rew = torch.empty(args.frames, n, device=dev)
         done = torch.empty(args.frames, n, device=dev, dtype=torch.bool)
         envs = {}
+        shared = VecDroneEnv(n, device=dev, config=cfg)
+        shared.reset()
         for v in args.variants.split(","):
-            e = VecDroneEnv(n, device=dev, config=cfg, library=abi.load(os.path.join(LAB, f"lib_{v}.so")))
-            e.reset()
+            # every variant steps the same buffers (physical placement out of the A/B)
+            e = VecDroneEnv.__new__(VecDroneEnv)
+            e.__dict__.update(shared.__dict__)
+            e._lib = abi.load(os.path.join(LAB, f"lib_{v}.so"))
             e.rollout(None if args.philox else acts, frames=args.frames, obs_out=obs, reward_out=rew, done_out=done,
                       write_obs=not args.no_obs)
             envs[v] = (e, [])
