@@ -435,17 +435,83 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
 // A frame for kernels that keep the lane's state in registers (the rollout
 // loops): the fast frame, and for a lane it reports risky the frame again
 // from the kept state with glibc's functions (a wave-uniform rare branch).
+#ifdef DD_EXP_EXACT_CALL
+struct ExactFrame {
+    Lane s;
+    double reward;
+};
+// by value: a Lane& would make the caller's state address-taken (scratch)
+template <bool kRef>
+__device__ __noinline__ ExactFrame frame_exact_call(const Consts* kp, const DDConfig* swp, uint32_t act, Lane s) {
+    const Consts& k = kRef ? kRefConsts : *kp;
+    ExactFrame r;
+    r.reward = frame<kRef, false, true>(k, kRef ? kRefConsts.c : *swp, act, s, nullptr);
+    r.s = s;
+    return r;
+}
+#endif
+
+#ifdef DD_EXP_EXACT_LDS
+struct ExactSlot {
+    double x, y, vx, vy, angle, omega, fuel, px, py, total, reward;
+    uint32_t status;
+    int32_t steps, episode;
+};
+typedef __attribute__((address_space(3))) ExactSlot* ExactSlotPtr;
+template <bool kRef>
+__device__ __noinline__ void frame_exact_lds(const Consts* kp, const DDConfig* swp, uint32_t act, ExactSlotPtr q) {
+    const Consts& k = kRef ? kRefConsts : *kp;
+    Lane s;
+    s.x = q->x; s.y = q->y; s.vx = q->vx; s.vy = q->vy; s.angle = q->angle; s.omega = q->omega;
+    s.fuel = q->fuel; s.px = q->px; s.py = q->py; s.total = q->total;
+    s.status = q->status; s.steps = q->steps; s.episode = q->episode;
+    s.speed = 0.0; s.dist = 0.0;
+    q->reward = frame<kRef, false, true>(k, kRef ? kRefConsts.c : *swp, act, s, nullptr);
+    q->x = s.x; q->y = s.y; q->vx = s.vx; q->vy = s.vy; q->angle = s.angle; q->omega = s.omega;
+    q->fuel = s.fuel; q->px = s.px; q->py = s.py; q->total = s.total;
+    q->status = s.status; q->steps = s.steps;
+}
+#endif
+
 template <bool kRef, bool kFlat>
 __device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
     const Lane s0 = s;
     bool risky = false;
     double reward = frame<kRef, kFlat>(k, sw, act, s, &risky);
+#ifdef DD_EXP_RISKY_ONLY
+    if (__builtin_expect(__ballot(risky) != 0, 0)) {
+        if (risky) reward = __builtin_nan("");
+    }
+#elif defined(DD_EXP_EXACT_LDS)
     if (__builtin_expect(__ballot(risky) != 0, 0)) {
         if (risky) {
-            s = s0;
-            reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
+            __shared__ ExactSlot slots[256];
+            ExactSlotPtr q = (ExactSlotPtr)&slots[threadIdx.x & 255];
+            q->x = s0.x; q->y = s0.y; q->vx = s0.vx; q->vy = s0.vy; q->angle = s0.angle; q->omega = s0.omega;
+            q->fuel = s0.fuel; q->px = s0.px; q->py = s0.py; q->total = s0.total;
+            q->status = s0.status; q->steps = s0.steps; q->episode = s0.episode;
+            frame_exact_lds<kRef>(kRef ? nullptr : &k, kRef ? nullptr : &sw, act, q);
+            s.x = q->x; s.y = q->y; s.vx = q->vx; s.vy = q->vy; s.angle = q->angle; s.omega = q->omega;
+            s.fuel = q->fuel; s.px = q->px; s.py = q->py; s.total = q->total;
+            s.status = q->status; s.steps = q->steps;
+            measure(s);
+            reward = q->reward;
         }
     }
+#elif !defined(DD_EXP_NO_EXACT)
+    if (__builtin_expect(__ballot(risky) != 0, 0)) {
+        if (risky) {
+#ifdef DD_EXP_EXACT_CALL
+            const ExactFrame e = frame_exact_call<kRef>(kRef ? nullptr : &k, kRef ? nullptr : &sw, act, s0);
+            s = e.s;
+            reward = e.reward;
+#else
+            s = s0;
+            reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
+#endif
+        }
+    }
+#endif
     return reward;
 }
 

@@ -57,6 +57,9 @@ for v in ${VARIANTS:-base}; do
     pad*) build $v -DDD_EXP_PAD_VALU=${v#pad} ;;
     glibctrig) build glibctrig -DDD_TRIG_GLIBC ;;
     noexact) build noexact -DDD_EXP_NO_EXACT ;;
+    exactcall) build exactcall -DDD_EXP_EXACT_CALL ;;
+    exactlds) build exactlds -DDD_EXP_EXACT_LDS ;;
+    riskyonly) build riskyonly -DDD_EXP_RISKY_ONLY ;;
     mpad*) build $v -DDD_MLP_PAD=${v#mpad} ;;
     log1p) build log1p -DDD_MLP_LOG1P ;;
     serial) build serial -DDD_MLP_SERIAL ;;
