@@ -628,11 +628,23 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
         slot = rollout_action<AFMT>(p, env, min(f + 2, p.frames - 1), i, pa);
         double reward;
         const bool was_done = (s.status & DD_ST_DONE) != 0;
+#ifdef DD_EXP_DEFER_REDO
+        constexpr bool kDefer = !kShaped;
+#else
+        constexpr bool kDefer = false;
+#endif
+        Lane s0;
+        bool risky = false;
+        if constexpr (kDefer) s0 = s;
+        auto fast = [&]() __attribute__((always_inline)) {
+            if constexpr (kDefer) return frame<kRef, true>(k, sw, act, s, &risky);
+            else return frame_checked<kRef, true>(k, sw, act, s);
+        };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
             // frame (a done lane's result is discarded), and a wave with a lane
             // to re-spawn takes the one branch
-            reward = frame_checked<kRef, true>(k, sw, act, s);
+            reward = fast();
             if (__ballot(was_done)) {
                 if (was_done) {
                     spawn(sw, k.c.max_fuel, env, s);
@@ -643,7 +655,7 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
             measure(s);
             reward = 0.0;
         } else {
-            reward = frame_checked<kRef, true>(k, sw, act, s);
+            reward = fast();
         }
         if constexpr (kShaped) {
             // dd_step's notebook path (finish_lane) with the history in h0 / h1:
@@ -681,6 +693,19 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
             put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
             put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
             if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+        }
+        if constexpr (kDefer) {
+            // the exact frame after the fast frame's outputs, which it rewrites
+            const bool redo = risky && !was_done;
+            if (__builtin_expect(__ballot(redo) != 0, 0)) {
+                if (redo) {
+                    s = s0;
+                    reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
+                    put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
+                    put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+                    if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+                }
+            }
         }
         quantize<T, kRef>(s);  // the obs above sees the unrounded frame, like dd_step's
         if constexpr (kObs) {

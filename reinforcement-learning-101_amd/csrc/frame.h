@@ -344,9 +344,14 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
             constexpr DDConfig r = reference_config();
             static_assert(-r.oob_margin == -50 && r.world_width + r.oob_margin == 850 && r.ground_level == 550,
                           "float boundary constants");
+            // |xf - 400| == 450 holds for xf = -50 and 850 (both subtractions
+            // exact), and for the few floats within 2^-15 of them that round
+            // onto it (harmless: a redo); likewise |yf - 250| == 300.  One
+            // compare instead of four compares and three mask ORs: the
+            // rollout loop is at its SGPR limit, and every lane mask costs one.
             const float xf = (float)s.x, yf = (float)s.y;
-            const bool q0 = xf == -50.0f, q1 = xf == 850.0f, q2 = yf == -50.0f, q3 = yf == 550.0f;
-            risky = q0 | q1 | q2 | q3;
+            const float qx = fabsf(fabsf(xf - 400.0f) - 450.0f), qy = fabsf(fabsf(yf - 250.0f) - 300.0f);
+            risky = fminf(qx, qy) == 0.0f;
         } else {
             const bool q0 = close(s.y, c.ground_level), q1 = close(s.x, -c.oob_margin),
                        q2 = close(s.x, c.world_width + c.oob_margin), q3 = close(s.y, -c.oob_margin);
@@ -387,9 +392,14 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
             on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
                      (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
             if constexpr (!kExact) {
-                const bool e0 = close(bx, s.px - c.platform_half_width), e1 = close(bx, s.px + c.platform_half_width),
-                           e2 = close(by, s.py - c.platform_half_height), e3 = close(by, s.py + c.platform_half_height);
-                risky |= e0 | e1 | e2 | e3;
+                // bx or by within 2^-20 (relative) of a pad edge: the nearest
+                // edge's distance against one bound that covers close() for
+                // every edge (|edge| <= |bx| + |by| + its distance), one compare
+                const double m = fmin(fmin(fabs(bx - (s.px - c.platform_half_width)),
+                                           fabs(bx - (s.px + c.platform_half_width))),
+                                      fmin(fabs(by - (s.py - c.platform_half_height)),
+                                           fabs(by - (s.py + c.platform_half_height))));
+                risky |= m <= 0x1p-19 * (1.0 + fabs(bx) + fabs(by));
             }
         }
     }

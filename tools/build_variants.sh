@@ -60,6 +60,7 @@ for v in ${VARIANTS:-base}; do
     exactcall) build exactcall -DDD_EXP_EXACT_CALL ;;
     exactlds) build exactlds -DDD_EXP_EXACT_LDS ;;
     riskyonly) build riskyonly -DDD_EXP_RISKY_ONLY ;;
+    defer) build defer -DDD_EXP_DEFER_REDO ;;
     mpad*) build $v -DDD_MLP_PAD=${v#mpad} ;;
     log1p) build log1p -DDD_MLP_LOG1P ;;
     serial) build serial -DDD_MLP_SERIAL ;;
