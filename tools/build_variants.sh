@@ -61,6 +61,9 @@ for v in ${VARIANTS:-base}; do
     exactlds) build exactlds -DDD_EXP_EXACT_LDS ;;
     riskyonly) build riskyonly -DDD_EXP_RISKY_ONLY ;;
     defer) build defer -DDD_EXP_DEFER_REDO ;;
+    maxilp) build maxilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
+    iterilp) build iterilp -mllvm -amdgpu-sched-strategy=iterative-ilp ;;
+    itermin) build itermin -mllvm -amdgpu-sched-strategy=iterative-minreg ;;
     mpad*) build $v -DDD_MLP_PAD=${v#mpad} ;;
     log1p) build log1p -DDD_MLP_LOG1P ;;
     serial) build serial -DDD_MLP_SERIAL ;;
