@@ -7,12 +7,17 @@
 // general OCML sincos spends ~100 VALU instructions on its fast path
 // (double-double Cody-Waite reduction sized for huge arguments); this one
 // spends ~40 for |x| < 2^19 * pi/2:
-//   * reduction: the classic two-round Cody-Waite split of pi/2 (33-bit head,
-//     so n * head is exact) good to ~118 bits, keeping the tail y1;
+//   * reduction: a three-part Cody-Waite split of pi/2 as three FMAs (33-bit
+//     head and middle, so n * head and n * middle are exact; the first FMA is
+//     exact, the second exact whenever it cancels, i.e. whenever the reduced
+//     argument is small enough for the tail to matter), no y1 tail word;
 //   * kernels: the public-domain fdlibm minimax polynomials (Sun, 1993) for
-//     sin and cos on [-pi/4, pi/4] with the tail correction; both are below
-//     1 ulp, the same accuracy class as glibc's correctly-rounded-in-practice
-//     sin/cos that the reference calls through numpy.
+//     sin and cos on [-pi/4, pi/4], without the tail correction.
+// Never more than 1 ulp from glibc's correctly-rounded-in-practice sin/cos
+// (the reference's, through numpy); 13 % of results are 1 ulp off (3 % with
+// the y1 tail kept, 16 VALU more: tests/test_trig_math.py).  The frame's
+// flags do not depend on it (near a boundary the lane is redone with glibc's
+// functions, frame.h), and an ulp of sin moves vx by an ulp of 0.15.
 // Beyond |x| = 2^19 * pi/2 (angles past 4.7e7 degrees, far outside anything
 // step() produces or the reference can normalise) the reduction loses
 // accuracy; no library fallback is compiled in, so the kernel carries no
@@ -53,36 +58,32 @@ DD_HD inline double hstep(double a, double z, double b) {
 #endif
 }
 
-// sin(y0 + y1), |y0 + y1| <= pi/4, |y1| tiny
-DD_HD inline double ksin(double x, double y) {
-    const double z = x * x;
-    const double v = z * x;
-    const double r = hstep(S2, z, hstep(S3, z, hstep(S4, z, hstep(S5, z, S6))));
-    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+// sin(y), |y| <= pi/4
+DD_HD inline double ksin(double y) {
+    const double z = y * y;
+    const double v = z * y;
+    const double r = hstep(S1, z, hstep(S2, z, hstep(S3, z, hstep(S4, z, hstep(S5, z, S6)))));
+    return fma(v, r, y);
 }
 
-// cos(y0 + y1), |y0 + y1| <= pi/4
-DD_HD inline double kcos(double x, double y) {
-    const double z = x * x;
+// cos(y), |y| <= pi/4
+DD_HD inline double kcos(double y) {
+    const double z = y * y;
     const double w = z * z;
     const double r = z * hstep(C1, z, hstep(C2, z, C3)) + w * w * hstep(C4, z, hstep(C5, z, C6));
     const double hz = 0.5 * z;
     const double u = 1.0 - hz;
-    return u + (((1.0 - u) - hz) + (z * r - x * y));
+    return u + (((1.0 - u) - hz) + z * r);
 }
 
-// (sin x, cos x), accurate (< 1 ulp) for |x| < 2^19 * pi/2.
+// (sin x, cos x), within 1 ulp for |x| < 2^19 * pi/2.
 DD_HD inline void sincos(double x, double* s, double* c) {
     const double fn = rint(x * kInvPio2);
     const int n = (int)fn;
-    const double t = x - fn * kPio2_1;  // exact: fn * head has <= 52 bits, Sterbenz
-    double w = fn * kPio2_2;            // exact (33-bit constant)
-    const double r = t - w;
-    w = fn * kPio2_2t - ((t - r) - w);
-    const double y0 = r - w;
-    const double y1 = (r - y0) - w;
-    const double sv = ksin(y0, y1);
-    const double cv = kcos(y0, y1);
+    const double t = fma(-fn, kPio2_1, x);  // exact: fn * head has <= 53 bits, Sterbenz
+    const double y = fma(-fn, kPio2_2t, fma(-fn, kPio2_2, t));
+    const double sv = ksin(y);
+    const double cv = kcos(y);
     // quadrant n & 3 -> (sv, cv), (cv, -sv), (-sv, -cv), (-cv, sv), as
     // selects and sign flips rather than a divergent switch
     const double a = (n & 1) ? cv : sv;
