@@ -384,6 +384,14 @@ int dd_abi_version(void);
  * bench.py reports PMC traffic only for the build it was measured on. */
 const char *dd_build_info(void);
 
+/* Self-check of the frame's square root (not a reference interface): the
+ * kernels take sqrt through an unscaled form of the compiler's sequence
+ * (trig.h sqrt_unscaled) for operands >= 2^-767.  Evaluates both on n
+ * doubles (the integers 0..2^20, then Philox-drawn values with exponents
+ * spread over the whole range) and adds the number whose results differ in
+ * any bit to *mismatches (device memory). */
+int dd_selftest_sqrt(uint64_t seed, int64_t n, unsigned long long *mismatches, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

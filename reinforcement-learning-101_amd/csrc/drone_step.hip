@@ -743,6 +743,43 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     }
 }
 
+// dd_selftest_sqrt kernel: trig::sqrt_unscaled against the compiler's sqrt()
+// on doubles from 2^-767 up, drawn with a uniform exponent (Philox bits: 11
+// exponent bits folded into [255, 2047), 52 random mantissa bits), plus the
+// integers 0..2^20 (spawn distances) at the start of the range; counts the
+// inputs whose results differ in any bit.
+__global__ __launch_bounds__(kBlock) void sqrt_selftest_kernel(uint64_t seed, uint64_t first, int64_t len,
+                                                               unsigned long long* mismatches) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint32_t r[4];
+    philox4x32_10((uint32_t)(first + 4 * t), (uint32_t)((first + 4 * t) >> 32), 0x5a17u, 0u, (uint32_t)seed,
+                  (uint32_t)(seed >> 32), r);
+    int bad = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t idx = 4 * t + q;
+        if ((int64_t)idx >= len) break;
+        const uint64_t g = first + idx;
+        double x;
+        if (g <= (1u << 20)) {
+            x = (double)g;
+        } else {
+            const uint32_t hi = r[q], lo = r[(q + 1) & 3] ^ r[(q + 2) & 3];
+            const uint64_t exp = 256u + (hi >> 21) % 1791u;  // [256, 2047): 2^-767 .. below inf
+            const uint64_t mant = ((uint64_t)(hi & 0xfffffu) << 32) | lo;
+            x = __builtin_bit_cast(double, (exp << 52) | mant);
+        }
+        const double a = sqrt(x), b = trig::sqrt_unscaled(x);
+        bad += __builtin_bit_cast(uint64_t, a) != __builtin_bit_cast(uint64_t, b);
+    }
+    const uint64_t m = __ballot(bad != 0);
+    if (m) {
+        int total = bad;
+        for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
+        if ((threadIdx.x & (kWave - 1)) == __ffsll((unsigned long long)m) - 1) atomicAdd(mismatches, (unsigned long long)total);
+    }
+}
+
 // dd_shaped_reset kernel: the notebook reward's history restarts from the
 // current state (slot 0 = its distance, slot 1 = none).
 template <typename T>
@@ -1166,6 +1203,19 @@ int dd_gae(const float* rewards, const float* values, const uint8_t* dones, floa
     const float gl = (float)(gamma * lambda);
     hipLaunchKernelGGL(dd::gae_kernel, dim3((unsigned)dd::tiles_of(n)), dim3(dd::kBlock), 0, s, rewards, values,
                        dones, advantages, returns, (int32_t)T, n, g, gl);
+    return dd::finish();
+}
+
+int dd_selftest_sqrt(uint64_t seed, int64_t n, unsigned long long* mismatches, void* stream) {
+    if (n < 0 || n > ((int64_t)1 << 40) || !mismatches) return hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t per = (int64_t)dd::kBlock * 4096;  // lanes per launch; 4 draws per lane
+    for (int64_t first = 0; first < n; first += per * 4) {
+        const int64_t len = n - first < per * 4 ? n - first : per * 4;
+        const unsigned blocks = (unsigned)dd::tiles_of((len + 3) / 4);
+        hipLaunchKernelGGL(dd::sqrt_selftest_kernel, dim3(blocks), dim3(dd::kBlock), 0, s, seed,
+                           (uint64_t)first, len, mismatches);
+    }
     return dd::finish();
 }
 

@@ -50,7 +50,10 @@ constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
 // the fast one: DD_TRIG_GLIBC (glibc's everywhere: +9 % step, +26 % rollout
 // with the table in global memory), DD_TRIG_OCML (the ROCm device
 // library's), DD_EXP_FAKE_TRIG (timing only).
-template <bool kExact = false>
+// kSgpr: the polynomial coefficients as SGPR operands (trig::hstep_c), for
+// the step kernel, whose four waves per SIMD overlap one wave's scalar moves
+// with another's VALU; the loops (one wave per SIMD) keep the vector form.
+template <bool kExact = false, bool kSgpr = false>
 __device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
     if constexpr (kExact) {
         libm::sincos(deg * kDeg2Rad, s, c);
@@ -63,8 +66,10 @@ __device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
     ::sincos(deg * kDeg2Rad, s, c);
 #elif defined(DD_TRIG_GLIBC)
     libm::sincos(deg * kDeg2Rad, s, c);
+#elif defined(DD_EXP_TRIG_VCOEF)
+    trig::sincos<false>(deg * kDeg2Rad, s, c);
 #else
-    trig::sincos(deg * kDeg2Rad, s, c);
+    trig::sincos<kSgpr>(deg * kDeg2Rad, s, c);
 #endif
 }
 
@@ -191,15 +196,40 @@ struct Lane {
 // may differ from the reference's by an ulp (the observation and the shaping
 // reward's tolerance); the one flag they decide, slow, is made exact in
 // frame().
+// kUnscaled (the step kernel): the two square roots go through
+// trig::sqrt_unscaled unless a lane of the wave has an operand below 2^-767
+// (zero included: a wave-uniform rare branch to sqrt()); bit-identical to
+// sqrt() either way (dd_selftest_sqrt).  Config 3: 8.13 -> 8.02 us per step
+// (lab medians, with the SGPR coefficients and the kRef thrust).  The loops
+// keep sqrt(): their frame is one basic block, and the branch splitting it
+// cost more than the four VALU it saves per root (65,536 x 256 rollout
+// 0.362 -> 0.371 ms, profiles/r03/lab/valu_trims_ab.jsonl).  DD_SQRT_LLVM:
+// sqrt() everywhere, for A/B runs.
+template <bool kUnscaled = false>
 __device__ __forceinline__ double measure(Lane& s) {
     const double dx = s.px - s.x, dy = s.py - s.y;
     const double ss = s.vx * s.vx + s.vy * s.vy;
+    const double dd = dx * dx + dy * dy;
 #ifdef DD_EXP_FAKE_SQRT  // timing-only sensitivity: what the two square roots cost
     s.speed = ss * 0.25;
-    s.dist = (dx * dx + dy * dy) * 0.001;
+    s.dist = dd * 0.001;
 #else
-    s.speed = sqrt(ss);
-    s.dist = sqrt(dx * dx + dy * dy);
+#ifndef DD_SQRT_LLVM
+    if (!kUnscaled) {
+#endif
+        s.speed = sqrt(ss);
+        s.dist = sqrt(dd);
+        return ss;
+#ifndef DD_SQRT_LLVM
+    }
+    if (__builtin_expect(__ballot(!(ss >= 0x1p-767) | !(dd >= 0x1p-767)) != 0, 0)) {
+        s.speed = sqrt(ss);
+        s.dist = sqrt(dd);
+    } else {
+        s.speed = trig::sqrt_unscaled(ss);
+        s.dist = trig::sqrt_unscaled(dd);
+    }
+#endif
 #endif
     return ss;
 }
@@ -234,7 +264,16 @@ __device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_
     s.status = 0u;  // not done / landed / crashed; platform direction +1
     s.steps = 0;
     s.total = 0.0;
-    measure(s);
+    // measure() of this state: the speed is sqrt(+0) = +0; the positions are
+    // integers (DDConfig's spawn fields), so the squared distance is 0 or at
+    // least 1, inside trig::sqrt_unscaled's exact range
+    const double dx = s.px - s.x, dy = s.py - s.y;
+    s.speed = 0.0;
+#if defined(DD_SQRT_LLVM) || defined(DD_EXP_FAKE_SQRT)
+    s.dist = sqrt(dx * dx + dy * dy);
+#else
+    s.dist = trig::sqrt_unscaled(dx * dx + dy * dy);
+#endif
 }
 
 // physics.normalize_angle after one frame's turn.  |omega| stays near
@@ -271,14 +310,32 @@ template <bool kRef, bool kFlat, bool kExact = false>
 __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s, bool* risky_out) {
     const DDConfig& c = k.c;
 
-    // apply_thrust: each thruster gated on fuel > 0 at that moment, in order
+    // apply_thrust: each thruster gated on fuel > 0 at that moment, in order.
+    // rotate_point(0, ty, angle) = (0 * ca - ty * sa, 0 * sa + ty * ca)
+    // (physics.py:6-23).  Under kRef (ty = -0.6) the zero products drop out
+    // exactly: ca and ty * ca are finite and nonzero (cos has no double
+    // zero), so 0 * sa + ty * ca = ty * ca; 0 * ca is +0 whenever ty * sa
+    // can be zero (sa = +-0 only at angle +-0, where ca = 1), so
+    // 0 * ca - ty * sa = 0.6 * sa + 0.0 (the +0.0 turns sa = -0's -0 into
+    // the reference's +0; a NaN angle gives NaN both ways).  3 f64 ops fewer.
     const double ty = -c.main_thrust_power;
+    constexpr bool kSgpr = !kFlat;  // the step kernel (trig::hstep_c)
+    const auto thrust = [&](double sa, double ca, double* dvx, double* dvy) __attribute__((always_inline)) {
+        if constexpr (kRef) {
+            *dvx = c.main_thrust_power * sa + 0.0;
+            *dvy = ty * ca;
+        } else {
+            *dvx = 0.0 * ca - ty * sa;
+            *dvy = 0.0 * sa + ty * ca;
+        }
+    };
     const bool main_on = (act & 1u) && s.fuel > 0.0;
     if constexpr (kFlat) {
-        double sa, ca;
+        double sa, ca, dvx, dvy;
         sincos_deg<kExact>(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
-        s.vx = main_on ? s.vx + (0.0 * ca - ty * sa) : s.vx;
-        s.vy = main_on ? s.vy + (0.0 * sa + ty * ca) : s.vy;
+        thrust(sa, ca, &dvx, &dvy);
+        s.vx = main_on ? s.vx + dvx : s.vx;
+        s.vy = main_on ? s.vy + dvy : s.vy;
         s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
         const bool left_on = (act & 2u) && s.fuel > 0.0;
         s.omega = left_on ? s.omega - c.side_thrust_power : s.omega;
@@ -288,10 +345,11 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
     } else {
         if (main_on) {
-            double sa, ca;
-            sincos_deg<kExact>(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)
-            s.vx += 0.0 * ca - ty * sa;
-            s.vy += 0.0 * sa + ty * ca;
+            double sa, ca, dvx, dvy;
+            sincos_deg<kExact, kSgpr>(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)
+            thrust(sa, ca, &dvx, &dvy);
+            s.vx += dvx;
+            s.vy += dvy;
             s.fuel -= c.fuel_main;
         }
         if ((act & 2u) && s.fuel > 0.0) { s.omega -= c.side_thrust_power; s.fuel -= c.fuel_side; }
@@ -359,7 +417,7 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         }
     }
 
-    const double ss = measure(s);  // speed (get_speed), distance (physics.distance), shared with get_state
+    const double ss = measure<!kFlat>(s);  // speed (get_speed), distance (physics.distance), shared with get_state
     const bool upright = fabs(s.angle) <= c.max_landing_angle;
     bool on_pad = false;  // _check_landing: bottom centre on the platform, slow and upright
     const double rx = c.platform_half_width + fabs(c.drone_half_height);
@@ -386,7 +444,7 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         }
         if (slow) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
             double sb, cb;
-            sincos_deg<kExact>(s.angle, &sb, &cb);
+            sincos_deg<kExact, kSgpr>(s.angle, &sb, &cb);
             const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
             const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
             on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &

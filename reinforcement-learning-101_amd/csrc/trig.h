@@ -58,32 +58,55 @@ DD_HD inline double hstep(double a, double z, double b) {
 #endif
 }
 
+// The same Horner step with the constant `a` as an SGPR operand of a VOP3
+// v_fma_f64 (device code, kSgpr).  Left to itself the compiler materialises
+// each coefficient into the accumulator with two v_mov_b32 and issues a
+// v_fmac: three VALU per step.  Here the two moves are s_mov (the scalar
+// unit, which another wave's VALU issue overlaps): the step kernel, four
+// waves per SIMD.  Same operation, same bits.  The innermost step of each
+// chain (two constants) keeps the plain form: a VOP3 reads one SGPR pair.
+template <bool kSgpr>
+DD_HD inline double hstep_c(double a, double z, double b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(DD_TRIG_NO_FMA)
+    if constexpr (kSgpr) {
+        double r;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(b), "s"(a));
+        return r;
+    }
+#endif
+    return hstep(a, z, b);
+}
+
 // sin(y), |y| <= pi/4
+template <bool kSgpr = false>
 DD_HD inline double ksin(double y) {
     const double z = y * y;
     const double v = z * y;
-    const double r = hstep(S1, z, hstep(S2, z, hstep(S3, z, hstep(S4, z, hstep(S5, z, S6)))));
+    const double r =
+        hstep_c<kSgpr>(S1, z, hstep_c<kSgpr>(S2, z, hstep_c<kSgpr>(S3, z, hstep_c<kSgpr>(S4, z, hstep(S5, z, S6)))));
     return fma(v, r, y);
 }
 
 // cos(y), |y| <= pi/4
+template <bool kSgpr = false>
 DD_HD inline double kcos(double y) {
     const double z = y * y;
     const double w = z * z;
-    const double r = z * hstep(C1, z, hstep(C2, z, C3)) + w * w * hstep(C4, z, hstep(C5, z, C6));
+    const double r = z * hstep_c<kSgpr>(C1, z, hstep(C2, z, C3)) + w * w * hstep_c<kSgpr>(C4, z, hstep(C5, z, C6));
     const double hz = 0.5 * z;
     const double u = 1.0 - hz;
     return u + (((1.0 - u) - hz) + z * r);
 }
 
 // (sin x, cos x), within 1 ulp for |x| < 2^19 * pi/2.
+template <bool kSgpr = false>
 DD_HD inline void sincos(double x, double* s, double* c) {
     const double fn = rint(x * kInvPio2);
     const int n = (int)fn;
     const double t = fma(-fn, kPio2_1, x);  // exact: fn * head has <= 53 bits, Sterbenz
     const double y = fma(-fn, kPio2_2t, fma(-fn, kPio2_2, t));
-    const double sv = ksin(y);
-    const double cv = kcos(y);
+    const double sv = ksin<kSgpr>(y);
+    const double cv = kcos<kSgpr>(y);
     // quadrant n & 3 -> (sv, cv), (cv, -sv), (-sv, -cv), (-cv, sv), as
     // selects and sign flips rather than a divergent switch
     const double a = (n & 1) ? cv : sv;
@@ -91,6 +114,33 @@ DD_HD inline void sincos(double x, double* s, double* c) {
     *s = (n & 2) ? -a : a;
     *c = ((n + 1) & 2) ? -b : b;
 }
+
+#if defined(__HIPCC__)
+// sqrt(x), correctly rounded, for x >= 2^-767, +-0, +inf and NaN: the
+// instruction sequence ROCm's compiler emits for a double sqrt on gfx950
+// (v_rsq_f64, then Goldschmidt / Newton refinements), without the scaling
+// it wraps around them for inputs below 2^-767 (a compare, two selects and
+// two v_ldexp_f64 per call).  For every input at or above 2^-767 the scaled
+// and unscaled sequences are the same operations on the same operand, so
+// the results are bit-identical; callers send smaller inputs to sqrt().
+__device__ __forceinline__ double sqrt_unscaled(double x) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    return sqrt(x);  // the host pass never runs device code
+#else
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return __builtin_amdgcn_class(x, 0x260) ? x : g;  // +-0 and +inf pass through
+#endif
+}
+#endif
 
 // x / d, correctly rounded, in three double ops instead of the ~10 of the
 // general division sequence.  inv_d = RN(1/d); q0 = RN(x * inv_d) is a

@@ -150,7 +150,12 @@ EXPORTS = {
     "dd_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dd_abi_version": (ctypes.c_int, []),
     "dd_build_info": (ctypes.c_char_p, []),
+    "dd_selftest_sqrt": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
+
+#: symbols a timing-only lab build (tools/build_variants.sh) or an older
+#: committed source built for an A/B run may lack
+_LAB_OPTIONAL = ("dd_build_info", "dd_selftest_sqrt")
 
 
 class NativeLibraryError(RuntimeError):
@@ -176,8 +181,8 @@ def load(path: str) -> ctypes.CDLL:
     except OSError as exc:  # pragma: no cover - depends on the box
         raise NativeLibraryError(f"cannot load {path}: {exc}") from exc
     for name, (restype, argtypes) in EXPORTS.items():
-        if name == "dd_build_info" and not hasattr(handle, name):
-            continue  # a timing-only lab build (tools/build_variants.sh) links no build record
+        if name in _LAB_OPTIONAL and not hasattr(handle, name):
+            continue
         fn = getattr(handle, name)
         fn.restype = restype
         fn.argtypes = argtypes

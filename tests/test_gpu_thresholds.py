@@ -69,3 +69,19 @@ def test_flags_exact_near_every_boundary(precision, gpu_device):
         for f in gd.FLOAT_FIELDS:
             assert gd.f32_close(host(getattr(env, f)), getattr(o, f), 1.0).all(), f
     assert gd.f32_close(host(obs), oobs, 1.0).all()
+
+
+def test_unscaled_sqrt_bit_equal_to_compiler_sqrt(gpu_device):
+    """The frame's square roots (speed, distance: drone.py:139-145,
+    physics.py:42-44) skip the compiler's scaling of inputs below 2^-767
+    (trig.h sqrt_unscaled; smaller ones take sqrt()).  On the device, every
+    integer 0..2^20 and 2^26 doubles with exponents spread from 2^-767 to the
+    largest finite give the same bits both ways."""
+    from delivery_drone_amd import abi
+    lib = abi.lib()
+    bad = torch.zeros(1, dtype=torch.int64, device=gpu_device)
+    stream = torch.cuda.current_stream(gpu_device).cuda_stream
+    rc = lib.dd_selftest_sqrt(12345, 1 << 26, bad.data_ptr(), stream)
+    assert rc == 0, abi.lib().dd_error_string(rc)
+    torch.cuda.synchronize(gpu_device)
+    assert int(bad.item()) == 0

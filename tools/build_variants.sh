@@ -57,6 +57,8 @@ for v in ${VARIANTS:-base}; do
     pad*) build $v -DDD_EXP_PAD_VALU=${v#pad} ;;
     glibctrig) build glibctrig -DDD_TRIG_GLIBC ;;
     noexact) build noexact -DDD_EXP_NO_EXACT ;;
+    sqrtllvm) build sqrtllvm -DDD_SQRT_LLVM ;;
+    vcoef) build vcoef -DDD_EXP_TRIG_VCOEF ;;
     exactcall) build exactcall -DDD_EXP_EXACT_CALL ;;
     exactlds) build exactlds -DDD_EXP_EXACT_LDS ;;
     riskyonly) build riskyonly -DDD_EXP_RISKY_ONLY ;;
