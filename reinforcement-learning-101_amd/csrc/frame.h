@@ -243,8 +243,15 @@ __device__ __forceinline__ double measure(Lane& s) {
 __device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_t env, Lane& s) {
     s.episode += 1;
     uint32_t r[4];
+#ifdef DD_EXP_FAKE_SPAWN  // timing-only sensitivity: what the re-spawn's Philox block costs
+    r[0] = (uint32_t)env * 0x9E3779B9u ^ (uint32_t)s.episode;
+    r[1] = r[0] * 0x85EBCA6Bu;
+    r[2] = r[1] * 0xC2B2AE35u;
+    r[3] = r[2] * 0x27D4EB2Fu;
+#else
     philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)s.episode, 0u,
                   (uint32_t)c.seed, (uint32_t)(c.seed >> 32), r);
+#endif
     if (c.randomize_drone) {
         s.x = draw_range(r[0], c.drone_x_min, (uint32_t)(c.drone_x_max - c.drone_x_min + 1));
         s.y = draw_range(r[1], c.drone_y_min, (uint32_t)(c.drone_y_max - c.drone_y_min + 1));
