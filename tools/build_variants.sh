@@ -60,6 +60,7 @@ for v in ${VARIANTS:-base}; do
     sqrtllvm) build sqrtllvm -DDD_SQRT_LLVM ;;
     vcoef) build vcoef -DDD_EXP_TRIG_VCOEF ;;
     fakespawn) build fakespawn -DDD_EXP_FAKE_SPAWN ;;
+    nolicm) build nolicm -mllvm -disable-machine-licm ;;
     exactcall) build exactcall -DDD_EXP_EXACT_CALL ;;
     exactlds) build exactlds -DDD_EXP_EXACT_LDS ;;
     riskyonly) build riskyonly -DDD_EXP_RISKY_ONLY ;;
