@@ -125,6 +125,9 @@ def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
         "host_cores": os.cpu_count(),
         "affinity_cores": len(os.sched_getaffinity(0)),
         "cpu_model": model,
+        "cores_note": ("workers = min(16, affinity) unless --cpu-workers: the GPU pool gives a one-GPU box a "
+                       "16-CPU share (OMP_NUM_THREADS/MAX_JOBS=16 there) although os.cpu_count() shows the "
+                       "whole host; per_core is the leg's value / workers"),
         "legs": legs,
         "sample": (f"config-3 workload, {workers} processes per leg on {model} (host: {os.cpu_count()} CPUs, "
                    f"{len(os.sched_getaffinity(0))} in this process's affinity). value = python_objects: "
@@ -888,7 +891,8 @@ def pmc_traffic_row(n: int, precision: str, obs: bool, path: str | None = None):
                 return None, "PMC row has no build_info (measured on an older build)"
             if dict(kv.split("=", 1) for kv in got.split(";")).get("step_isa") != step_isa:
                 return None, f"PMC row measured on step_isa of '{got}', this library is '{have}'"
-            return r.get("hbm_bytes_per_launch"), f"PMC FETCH_SIZE/WRITE_SIZE passes on build {got}"
+            return r.get("hbm_bytes_per_launch"), (f"PMC FETCH_SIZE/WRITE_SIZE passes of the step kernel; its ISA "
+                                                   f"(step_isa={step_isa}) matches this library's")
     return None, f"no PMC row for envs={n} precision={precision} obs={obs}"
 
 

@@ -965,10 +965,21 @@ __global__ __launch_bounds__(kBlock) void compact_scatter_kernel(const uint8_t* 
 inline int64_t tiles_of(int64_t n) { return (n + kBlock - 1) / kBlock; }
 
 
+// Lab switches (timing-only builds, tools/build_variants.sh): unused dynamic
+// LDS per block, which caps the blocks a CU takes and so spreads a launch
+// over more CUs.  0 in the product.
+#ifndef DD_EXP_STEP_DYN_LDS
+#define DD_EXP_STEP_DYN_LDS 0
+#endif
+#ifndef DD_EXP_ROLL_DYN_LDS
+#define DD_EXP_ROLL_DYN_LDS 0
+#endif
+
 template <typename T, int AFMT, bool kRef, bool kShaped>
 void launch_step(const StepArgs& p, const Soa<T>& a, hipStream_t s) {
     const unsigned blocks = (unsigned)((p.n + kStepBlock - 1) / kStepBlock);
-    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShaped>), dim3(blocks), dim3(kStepBlock), 0, s, p, a);
+    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShaped>), dim3(blocks), dim3(kStepBlock), DD_EXP_STEP_DYN_LDS, s,
+                       p, a);
 }
 
 template <typename T, bool kRef, bool kShaped>
@@ -1015,9 +1026,11 @@ void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
     const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0;
     const unsigned blocks = (unsigned)tiles_of(p.n);
     if (held)
-        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true, kShaped>), dim3(blocks), dim3(kBlock), 0, s, p, a);
+        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true, kShaped>), dim3(blocks), dim3(kBlock),
+                           DD_EXP_ROLL_DYN_LDS, s, p, a);
     else
-        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false, kShaped>), dim3(blocks), dim3(kBlock), 0, s, p, a);
+        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false, kShaped>), dim3(blocks), dim3(kBlock),
+                           DD_EXP_ROLL_DYN_LDS, s, p, a);
 }
 
 template <typename T, bool kRef, bool kShaped>

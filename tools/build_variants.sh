@@ -54,6 +54,8 @@ for v in ${VARIANTS:-base}; do
     tlwtsnto) build tlwtsnto -DDD_EXP_TIMELINE -DDD_ST_STATE=1 -DDD_ST_OUT=3 -DDD_ST_OBS=3 ;;
     tlwtall) build tlwtall -DDD_EXP_TIMELINE -DDD_ST_STATE=1 -DDD_ST_OUT=1 -DDD_ST_OBS=1 ;;
     ieeerstd) build ieeerstd -DDD_MLP_IEEE_RSTD ;;
+    sl*) build $v -DDD_EXP_STEP_DYN_LDS=${v#sl} ;;
+    rl*) build $v -DDD_EXP_ROLL_DYN_LDS=${v#rl} ;;
     pad*) build $v -DDD_EXP_PAD_VALU=${v#pad} ;;
     glibctrig) build glibctrig -DDD_TRIG_GLIBC ;;
     noexact) build noexact -DDD_EXP_NO_EXACT ;;
