@@ -37,6 +37,7 @@ def test_cpu_baseline_fields():
     assert r["value"] == r["legs"]["python_objects"]["value"]
     assert r["legs"]["c_scalar"]["value"] > r["legs"]["python_objects"]["value"]  # C beats Python objects
     assert r["host_cores"] == os.cpu_count() and r["affinity_cores"] >= 1 and r["cpu_model"]
+    assert "16" in r["cores_note"]  # why workers != host_cores on the GPU pool
 
 
 def test_pmc_traffic_only_for_the_measured_build(tmp_path):
@@ -54,7 +55,8 @@ def test_pmc_traffic_only_for_the_measured_build(tmp_path):
     v, note = b.pmc_traffic_row(262144, "f32", True, str(p))
     assert v is None and "step_isa" in note
     p.write_text(json.dumps({"rows": [dict(row, build_info=info)]}))
-    assert b.pmc_traffic_row(262144, "f32", True, str(p))[0] == 123
+    v, note = b.pmc_traffic_row(262144, "f32", True, str(p))
+    assert v == 123 and info.split(";")[1] in note  # the note names the matched step ISA
     assert b.pmc_traffic_row(4096, "f32", True, str(p))[0] is None
 
 
