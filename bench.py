@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--cpu-baseline", type=float, default=8.0,
                    help="seconds of CPU-baseline wall time per leg (0 = skip)")
     p.add_argument("--cpu-workers", type=int, default=0,
-                   help="CPU-baseline processes per leg (0 = min(16, CPUs in this process's affinity))")
+                   help="CPU-baseline processes per leg (0 = this process's CPU share: host_cpu_share())")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
@@ -62,6 +62,69 @@ def parse():
 
 
 # ----------------------------------------------------------------- CPU baseline
+def _cgroup_quota(root: str = "/sys/fs/cgroup", proc: str = "/proc/self/cgroup"):
+    """(cpus, file) from this process's cgroup CPU quota, or (None, why not).
+    cgroup v2: <root>/<path>/cpu.max = "<quota> <period>" ("max" = none);
+    cgroup v1: cpu.cfs_quota_us / cpu.cfs_period_us (quota -1 = none).  The
+    process's own cgroup directory is tried first, then the mount root (a
+    container's namespace root)."""
+    try:
+        lines = open(proc).read().split("\n")
+    except OSError as e:
+        return None, f"{proc}: {e.strerror}"
+    v2 = [l.split(":", 2)[2] for l in lines if l.startswith("0::")]
+    v1 = [l.split(":", 2)[2] for l in lines if l.count(":") >= 2 and "cpu" in l.split(":", 2)[1].split(",")]
+    cands = []
+    for rel in v2:
+        cands += [("v2", os.path.join(root, rel.lstrip("/")))]
+    for rel in v1:
+        for mnt in ("cpu", "cpu,cpuacct", "cpuacct,cpu"):
+            cands += [("v1", os.path.join(root, mnt, rel.lstrip("/"))), ("v1", os.path.join(root, mnt))]
+    cands += [("v2", root)]
+    seen = []
+    for kind, d in cands:
+        try:
+            if kind == "v2":
+                f = os.path.join(d, "cpu.max")
+                quota, period = open(f).read().split()[:2]
+                seen.append(f)
+                if quota != "max":
+                    return float(quota) / float(period), f
+            else:
+                f = os.path.join(d, "cpu.cfs_quota_us")
+                quota = int(open(f).read())
+                period = int(open(os.path.join(d, "cpu.cfs_period_us")).read())
+                seen.append(f)
+                if quota > 0:
+                    return quota / period, f
+        except (OSError, ValueError):
+            continue
+    return None, ("no CPU quota set (" + ", ".join(seen) + ")") if seen else "no cgroup CPU controller file readable"
+
+
+def host_cpu_share() -> dict:
+    """The CPUs the CPU baseline may use on this host, with the evidence
+    (the reference loop on the host's cores).  In order:
+    the cgroup CPU quota (quota / period, rounded down) when one is set;
+    otherwise the pool's declared per-job share, OMP_NUM_THREADS / MAX_JOBS
+    (the one-GPU box exports 16 and its operators ask worker pools to
+    follow it, since os.cpu_count() and the affinity show the whole host);
+    otherwise the CPUs in this process's affinity.  Never more than the
+    affinity."""
+    aff = len(os.sched_getaffinity(0))
+    quota, qsrc = _cgroup_quota()
+    env = {k: os.environ[k] for k in ("OMP_NUM_THREADS", "MAX_JOBS") if os.environ.get(k, "").isdigit()}
+    if quota is not None:
+        cores, src = max(1, int(quota)), f"cgroup quota {quota:g} CPUs ({qsrc})"
+    elif env:
+        k = min(env, key=lambda k: int(env[k]))
+        cores, src = int(env[k]), f"{k}={env[k]} (the job's declared CPU share; {qsrc})"
+    else:
+        cores, src = aff, f"sched_getaffinity ({qsrc})"
+    return {"cores": max(1, min(cores, aff)), "source": src, "cgroup_quota_cpus": quota,
+            "affinity_cores": aff, "host_cores": os.cpu_count(), "env": env}
+
+
 def _cpu_worker(args):
     leg, lane0, lanes, steps, seed = args
     from delivery_drone_amd.config import EnvConfig
@@ -94,7 +157,7 @@ def _cpu_leg(leg: str, seconds: float, workers: int, seed: int, lanes: int, cali
             "frames": steps, "drone_steps": total, "wall_s": round(wall, 2)}
 
 
-def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
+def cpu_baseline(seconds: float, workers: int, seed: int, share: dict | None = None) -> dict:
     """The reference's step on the host's cores, config-3 workload (random
     spawn, auto-reset, uniform random actions, observation every frame), a
     bounded sample of ~`seconds` per leg:
@@ -106,8 +169,10 @@ def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
     * c_scalar: oracle/drone_oracle.c, the fixture-pinned scalar f64 C
       restatement (what a native CPU port reaches).
 
-    `workers` processes per leg (default: the CPUs this process may run on,
-    capped at 16 — the GPU box's CPU share per GPU; --cpu-workers overrides)."""
+    `workers` processes per leg (default: host_cpu_share(), recorded with its
+    evidence as `cpu_share`; --cpu-workers overrides).  `value` is the
+    python_objects leg (`baseline_leg`); `speedup_basis` lists both legs so a
+    ratio against either stays comparable across rounds."""
     from oracle import oracle as ora
     ora.build()
     legs = {"python_objects": _cpu_leg("python_objects", seconds, workers, seed, 256, 8),
@@ -117,17 +182,20 @@ def cpu_baseline(seconds: float, workers: int, seed: int) -> dict:
     except (OSError, IndexError):
         model = platform.processor()
     py, c = legs["python_objects"], legs["c_scalar"]
+    share = share or host_cpu_share()
     return {
         "value": py["value"],
         "unit": "env-steps/s",
         "cores": workers,
         "kind": "port",
+        "baseline_leg": "python_objects",
+        "speedup_basis": {"python_objects": py["value"], "c_scalar": c["value"]},
         "host_cores": os.cpu_count(),
         "affinity_cores": len(os.sched_getaffinity(0)),
+        "cpu_share": share,
         "cpu_model": model,
-        "cores_note": ("workers = min(16, affinity) unless --cpu-workers: the GPU pool gives a one-GPU box a "
-                       "16-CPU share (OMP_NUM_THREADS/MAX_JOBS=16 there) although os.cpu_count() shows the "
-                       "whole host; per_core is the leg's value / workers"),
+        "cores_note": (f"workers = {workers}: " + (f"the CPU share, {share['source']}" if workers == share["cores"]
+                       else "--cpu-workers") + "; per_core is the leg's value / workers"),
         "legs": legs,
         "sample": (f"config-3 workload, {workers} processes per leg on {model} (host: {os.cpu_count()} CPUs, "
                    f"{len(os.sched_getaffinity(0))} in this process's affinity). value = python_objects: "
@@ -391,6 +459,29 @@ def reduce_max(values, backend, dev):
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(v) for v in t]
+
+
+def f64_point(n, seed, dev, steps=500, graph_steps=50):
+    """The headline workload (config 3: n drones, random spawn, auto-reset,
+    obs every frame) with the state stored at the reference's own width
+    (precision='f64', Python floats: drone.py:12-42): same arithmetic, 80 B
+    of state per drone instead of 40, bytes per env from
+    dd_step_bytes_per_env(DD_F64, ...)."""
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    env = VecDroneEnv(n, device=dev, config=cfg, precision="f64")
+    env.reset()
+    rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
+    ms = time_steps(env, rows, steps, graph_steps, torch.cuda.Stream(dev))
+    bpe = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=True)
+    assert bpe == abi.lib().dd_step_bytes_per_env(abi.DD_F64, abi.DD_ACT_BITMASK, 1)
+    gbs = bpe * n / (ms * 1e-3) / 1e9
+    del env, rows
+    torch.cuda.empty_cache()
+    return {"envs": n, "precision": "f64", "us_per_step": round(ms * 1e3, 3), "steps_per_s": round(n / (ms * 1e-3), 1),
+            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env": bpe,
+            "kernel": "dd::step_kernel<double, 0, true, false>", "launch": f"hipGraph of {graph_steps} dd_step"}
 
 
 def gae_point(n, frames, dev):
@@ -675,8 +766,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline > 0:
-        workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))
-        cpu = cpu_baseline(args.cpu_baseline, workers, args.seed)
+        share = host_cpu_share()
+        workers = args.cpu_workers or share["cores"]
+        cpu = cpu_baseline(args.cpu_baseline, workers, args.seed, share)
 
     import torch
     import torch.distributed as dist
@@ -777,7 +869,7 @@ def main():
             gp = gather_point(env.obs, n, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
             gp = {"error": f"{type(e).__name__}: {e}"[:300]}
-    c5 = c5a = g5 = c2 = nb = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None
+    c5 = c5a = g5 = c2 = nb = f64p = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         c5a = step_loop_point(args.rollout_point, 256, args.precision, args.seed, dev)
@@ -785,6 +877,7 @@ def main():
     if world == 1 and args.extra_points:
         c2 = config2_point(args.seed, dev)
         nb = notebook_point(n, args.precision, args.seed, dev)
+        f64p = f64_point(n, args.seed, dev)
         pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
         pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
         pp16 = policy_point(args.rollout_point or 65_536, args.seed, dev, "f16x3")
@@ -848,6 +941,7 @@ def main():
             "gather_point": gp,
             "gae_point": g5,
             "notebook_reward_point": nb,
+            "f64_point": f64p,
             "policy_point": pp,
             "policy_rollout_point": pr,
             "policy_point_f16x3": pp16,

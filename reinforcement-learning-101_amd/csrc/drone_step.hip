@@ -448,6 +448,7 @@ struct RolloutArgs {
     Consts k;
     const char* actions;      // frame 0, lane 0 of this chunk
     int64_t act_stride;       // bytes between frames (N x action width)
+    uint32_t act_bytes;       // extent of the launch's action rows from `actions` (< 2^32, see rollout_chunks)
     char* reward;             // frame 0, lane 0 of this chunk
     int64_t reward_stride;    // bytes between frames
     uint8_t* done;
@@ -525,51 +526,74 @@ __device__ __forceinline__ Soa<T> reload_soa() {
 // rows are read back into registers before frame f's arithmetic and stored
 // after it, so the LDS round trip and the stores overlap the frame instead
 // of following it (the rollout runs one wave per SIMD at 65,536 drones:
-// nothing else hides latency).  Every frame issues the same stores (4
-// predicated 16-byte stores + 1 predicated tail dword per lane), so the
-// vmcnt waits the compiler places for the action prefetch stay short.
+// nothing else hides latency).
 // !kHeld: one slice per wave, flushed after each frame.
 struct HeldObs {
     f32x4 v[4];  // a 64-row slice is 240 float4: 3.75 per lane
-    float tail;  // rows * 15 % 4 floats past the last whole float4 (ragged wave)
 };
 
 // Reads the whole 64-row slice at wtile (plus padding: the tile carries
 // kHeldPad floats past its last slice), unconditionally so the four reads
-// issue back to back; store_held_wave writes only the nf = rows * 15 floats
-// that are rows.
+// issue back to back; store_held_wave writes only the float4s that are rows.
 constexpr int kHeldPad = 4 * kWave * 4 - kWave * DD_OBS_DIM;  // 256 float4 read vs 240 in a slice
 
-__device__ __forceinline__ void hold_obs_wave(const float* wtile, int nf, HeldObs& h) {
+__device__ __forceinline__ void hold_obs_wave(const float* wtile, HeldObs& h) {
     const int lane = threadIdx.x & (kWave - 1);
     const f32x4* src4 = reinterpret_cast<const f32x4*>(wtile);
 #pragma unroll
     for (int j = 0; j < 4; ++j) h.v[j] = src4[lane + j * kWave];
-    h.tail = wtile[((nf >> 2) << 2) + (lane & 3)];
 }
 
-// dst is wave-uniform (SGPR base); a full slice (nf = 960: 240 float4) takes
-// three unpredicated stores and one for lanes < 48.
-__device__ __forceinline__ void store_held_wave(const HeldObs& h, float* dst, int nf) {
-    const int lane = threadIdx.x & (kWave - 1);
-    f32x4* dst4 = reinterpret_cast<f32x4*>(uniform_ptr(dst));
-    if (nf == kWave * DD_OBS_DIM) {
+// A raw buffer resource over [p, p + bytes): accesses at offsets >= bytes
+// are dropped (stores) or read 0 (loads) by the hardware's range check.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_over(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// The held slice leaves as four unconditional 16-byte non-temporal raw
+// buffer stores over the wave's slice of one frame (`slice` covers its rows
+// * 60 bytes): float4 lane + 64 j past the slice (lanes >= 48 of j = 3, all
+// of a ragged wave's missing rows) is dropped by the range check.  No
+// exec-mask branches, so every frame issues the same vector-memory
+// instructions and the compiler's vmcnt waits for the action prefetch count
+// exactly (with the branchy stores of rounds 1-3 it waited, at the end of
+// every frame pair, for that pair's own reward / done / obs stores:
+// SQ_WAIT_ANY 186 of 720 wave cycles per frame).  Under kHeld N % 4 == 0,
+// so a wave's slice is whole float4s.
+__device__ __forceinline__ void store_held_wave(const HeldObs& h, __amdgpu_buffer_rsrc_t slice) {
+    const uint32_t lane = threadIdx.x & (kWave - 1);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) store_obs4<DD_ST_OBS>(dst4, lane + j * kWave, h.v[j]);
-        if (lane < kWave * DD_OBS_DIM / 4 - 3 * kWave) store_obs4<DD_ST_OBS>(dst4, lane + 3 * kWave, h.v[3]);
-        return;
+    for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h.v[j]), slice, (lane + j * kWave) * 16u, 0,
+                                               2 /* nt */);
+}
+
+// One lane's action of one frame, by raw buffer loads over the launch's
+// [frames][N] action rows (rollout_chunks keeps every consumed offset below
+// 2^32): a prefetch past the last frame needs no clamp, the range check
+// makes it read 0.
+template <int AFMT>
+__device__ __forceinline__ uint32_t buffer_action(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    if constexpr (AFMT == DD_ACT_BITMASK) {
+        return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+    } else if constexpr (AFMT == DD_ACT_F32X3) {
+        const float a0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+        const float a1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0));
+        const float a2 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off + 8u, 0, 0));
+        return (a0 != 0.0f ? 1u : 0u) | (a1 != 0.0f ? 2u : 0u) | (a2 != 0.0f ? 4u : 0u);
+    } else {
+        const uint32_t a0 = __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+        const uint32_t a1 = __builtin_amdgcn_raw_buffer_load_b8(r, off + 1u, 0, 0);
+        const uint32_t a2 = __builtin_amdgcn_raw_buffer_load_b8(r, off + 2u, 0, 0);
+        return (a0 ? 1u : 0u) | (a1 ? 2u : 0u) | (a2 ? 4u : 0u);
     }
-    const int nv = nf >> 2;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int k = lane + j * kWave;
-        if (k < nv) __builtin_nontemporal_store(h.v[j], &dst4[k]);
-    }
-    if (lane < (nf & 3)) __builtin_nontemporal_store(h.tail, dst + (nv << 2) + lane);
 }
 
 #ifndef DD_ROLL_MIN_WAVES
-#define DD_ROLL_MIN_WAVES 1  // per SIMD; 4 caps the kernel at 128 VGPRs (A/B: DESIGN.md section 4)
+// per SIMD: 2 keeps the kernel within 256 registers in all (1 let the Philox-action
+// variant take 2 AGPRs on top of 256 VGPRs, one wave per SIMD at 262,144 drones:
+// +38 %); 4 caps it at 128 VGPRs and spills (A/B: DESIGN.md section 4)
+#define DD_ROLL_MIN_WAVES 2
 #endif
 template <typename T, int AFMT, bool kRef, bool kHeld, bool kShaped>
 __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(RolloutArgs p, Soa<T> a) {
@@ -586,7 +610,6 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     // this wave's first row, its row count and slice offset: wave-uniform, in SGPRs
     const uint32_t wrow0 = __builtin_amdgcn_readfirstlane(row0 + (threadIdx.x & ~(kWave - 1)));
     const int wrows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
-    const int wfloats = wrows * DD_OBS_DIM;
     const int woff = (int)__builtin_amdgcn_readfirstlane((threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM);
     const int roff = threadIdx.x * DD_OBS_DIM;                   // the lane's row in a tile
     const int64_t env = a.env_id_base + i;
@@ -601,14 +624,51 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     s.status = at(a.status, i);
     s.steps = at(a.steps, i);
     s.episode = at(a.episode, i);
-    // Actions are prefetched two frames ahead into two registers used in
-    // turn (the loop is unrolled by two, so no register copy of a pending
-    // load): the load a frame consumes was issued before two frames' stores,
-    // and its vmcnt wait is long met.
+    // Output streams as wave-uniform cursors advanced once per frame (SGPR
+    // pairs: two scalar adds each, where recomputing base + f * stride took
+    // six and the frame loop's SGPRs spilled), every store an SGPR base + the
+    // lane's 32-bit offset.  obs_prev: frame f - 1's slice of this wave (its
+    // range is empty at f = 0).
+    char* rew_p = p.reward;
+    uint8_t* done_p = p.done;
+    char* erew_p = p.engine_reward;  // (advanced every frame: test has_engine, not the pointer)
+    uint8_t* edone_p = p.engine_done;
+    const bool has_engine = p.engine_reward != nullptr;
+    const float* obs_prev = p.obs + ((int64_t)wrow0 - p.n_total) * DD_OBS_DIM;
+    const uint32_t slice_bytes = (uint32_t)wrows * (DD_OBS_DIM * 4);
+    uint32_t prev_bytes = 0;
+    // Actions: raw buffer loads (buffer_action), prefetched two frames ahead
+    // into two registers used in turn (the loop is unrolled by two, so no
+    // register copy of a pending load); act_next is the byte offset of the
+    // frame the next prefetch reads.
+    // kActDw (bitmask actions under kHeld, whose launch condition includes a
+    // 4-byte aligned action buffer and N % 4 == 0): the lane loads the
+    // aligned dword holding its byte and extracts it where the frame uses it.
+    // The prefetched value is then a plain 32-bit register; a loaded byte
+    // crosses the loop's back edge as a 16-bit value whose widening (a
+    // v_and 0xffff) the compiler placed at the loop latch, right behind the
+    // pair's stores, and waited there for the load.
+    constexpr bool kActDw = kHeld && AFMT == DD_ACT_BITMASK;
+    constexpr uint32_t act_w = AFMT == DD_ACT_F32X3 ? 12u : AFMT == DD_ACT_U8X3 ? 3u : 1u;
+    const __amdgpu_buffer_rsrc_t act_r = rsrc_over(p.actions, AFMT == DD_ACT_PHILOX ? 0u : p.act_bytes);
+    const uint32_t act_lane = kActDw ? (i & ~3u) : i * act_w;
+    const uint32_t act_sh = (i & 3u) * 8u;
+    const uint32_t act_stride = (uint32_t)p.act_stride;
+    uint32_t act_next = 0;
     uint32_t act0 = 0, act1 = 0;
     PhiloxActions pa;
-    if (p.frames > 0) act0 = rollout_action<AFMT>(p, env, 0, i, pa);
-    if (p.frames > 1) act1 = rollout_action<AFMT>(p, env, 1, i, pa);
+    if constexpr (AFMT == DD_ACT_PHILOX) {
+        act0 = rollout_action<AFMT>(p, env, 0, i, pa);
+        act1 = rollout_action<AFMT>(p, env, 1, i, pa);
+    } else if constexpr (kActDw) {
+        act0 = __builtin_amdgcn_raw_buffer_load_b32(act_r, act_lane, 0, 0);
+        act1 = __builtin_amdgcn_raw_buffer_load_b32(act_r, act_lane + act_stride, 0, 0);
+        act_next = 2u * act_stride;
+    } else {
+        act0 = buffer_action<AFMT>(act_r, act_lane);
+        act1 = buffer_action<AFMT>(act_r, act_lane + act_stride);
+        act_next = 2u * act_stride;
+    }
     // every prologue load lands here, not at a wait inside the frame loop
     asm volatile("" ::"v"(s.x), "v"(s.y), "v"(s.vx), "v"(s.vy), "v"(s.angle), "v"(s.omega), "v"(s.fuel),
                  "v"(s.px), "v"(s.py), "v"(s.total), "v"(s.status), "v"(s.steps), "v"(s.episode), "v"(act0),
@@ -617,29 +677,23 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     // body carries no uniform branch on them.
     auto run_frame = [&](const int f, uint32_t& slot, auto obs_c, auto auto_c) __attribute__((always_inline)) {
         constexpr bool kObs = decltype(obs_c)::value, kAuto = decltype(auto_c)::value;
-        if (kHeld && kObs && f > 0) {
+        if (kHeld && kObs) {
             __syncwarp();  // frame f - 1's rows (other lanes of this wave) are in LDS
-            hold_obs_wave(tile[(f - 1) & 1] + woff, wfloats, held);
+            hold_obs_wave(tile[(f - 1) & 1] + woff, held);
         }
-        // unconditional (the last two frames re-read the last row): a
-        // conditional load would leave a register copy of it, and that copy
-        // waits for the load
-        const uint32_t act = slot;
-        slot = rollout_action<AFMT>(p, env, min(f + 2, p.frames - 1), i, pa);
+        const uint32_t act = kActDw ? __builtin_amdgcn_ubfe(slot, act_sh, 3) : slot;
+        if constexpr (AFMT == DD_ACT_PHILOX) {
+            slot = rollout_action<AFMT>(p, env, f + 2, i, pa);
+        } else if constexpr (kActDw) {
+            slot = __builtin_amdgcn_raw_buffer_load_b32(act_r, act_lane + act_next, 0, 0);
+            act_next += act_stride;
+        } else {
+            slot = buffer_action<AFMT>(act_r, act_lane + act_next);
+            act_next += act_stride;
+        }
         double reward;
         const bool was_done = (s.status & DD_ST_DONE) != 0;
-#ifdef DD_EXP_DEFER_REDO
-        constexpr bool kDefer = !kShaped;
-#else
-        constexpr bool kDefer = false;
-#endif
-        Lane s0;
-        bool risky = false;
-        if constexpr (kDefer) s0 = s;
-        auto fast = [&]() __attribute__((always_inline)) {
-            if constexpr (kDefer) return frame<kRef, true>(k, sw, act, s, &risky);
-            else return frame_checked<kRef, true>(k, sw, act, s);
-        };
+        auto fast = [&]() __attribute__((always_inline)) { return frame_checked<kRef, true>(k, sw, act, s); };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
             // frame (a done lane's result is discarded), and a wave with a lane
@@ -682,44 +736,43 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
                     s.status |= DD_ST_DONE;
                 }
             }
-            put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)shaped);
-            put_out(p.done + f * p.n_total, i, (uint8_t)(shaped_done ? 1 : 0));
-            if (p.engine_reward) {
-                put_out(reinterpret_cast<T*>(p.engine_reward + f * p.reward_stride), i, (T)reward);
-                put_out(p.engine_done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+            put_out(reinterpret_cast<T*>(rew_p), i, (T)shaped);
+            put_out(done_p, i, (uint8_t)(shaped_done ? 1 : 0));
+            if (has_engine) {
+                put_out(reinterpret_cast<T*>(erew_p), i, (T)reward);
+                put_out(edone_p, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
             }
-            if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
         } else {
-            put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
-            put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-            if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+            put_out(reinterpret_cast<T*>(rew_p), i, (T)reward);
+            put_out(done_p, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
         }
-        if constexpr (kDefer) {
-            // the exact frame after the fast frame's outputs, which it rewrites
-            const bool redo = risky && !was_done;
-            if (__builtin_expect(__ballot(redo) != 0, 0)) {
-                if (redo) {
-                    s = s0;
-                    reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
-                    put_out(reinterpret_cast<T*>(p.reward + f * p.reward_stride), i, (T)reward);
-                    put_out(p.done + f * p.n_total, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-                    if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
-                }
-            }
-        }
+        if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
         quantize<T, kRef>(s);  // the obs above sees the unrounded frame, like dd_step's
         if constexpr (kObs) {
             if constexpr (kHeld) {
-                if (f > 0) store_held_wave(held, p.obs + ((size_t)(f - 1) * p.n_total + wrow0) * DD_OBS_DIM, wfloats);
+                store_held_wave(held, rsrc_over(obs_prev, prev_bytes));  // frame f - 1's rows
+                prev_bytes = slice_bytes;
+                obs_prev += p.n_total * DD_OBS_DIM;
             } else {
                 flush_obs_wave(tile[0] + woff, p.obs + ((size_t)f * p.n_total + wrow0) * DD_OBS_DIM, wrows);
             }
         }
+        rew_p += p.reward_stride;
+        done_p += p.n_total;
+        if constexpr (kShaped) {
+            erew_p += p.reward_stride;
+            edone_p += p.n_total;
+        }
     };
     auto run = [&](auto obs_c, auto auto_c) __attribute__((always_inline)) {
+        // an odd count leaves the loop between the pair's frames (`break`, not
+        // a skipped second frame): the loop latch is then reached from one
+        // path only, and the vmcnt the compiler derives there for the
+        // prefetched actions counts every store the pair issued
         for (int f = 0; f < p.frames; f += 2) {
             run_frame(f, act0, obs_c, auto_c);
-            if (f + 1 < p.frames) run_frame(f + 1, act1, obs_c, auto_c);
+            if (f + 1 >= p.frames) break;
+            run_frame(f + 1, act1, obs_c, auto_c);
         }
     };
     using yes = std::true_type;
@@ -734,8 +787,8 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     if (kHeld && p.obs && p.frames > 0) {  // the last frame's slice
         const int f = p.frames - 1;
         __syncwarp();
-        hold_obs_wave(tile[f & 1] + woff, wfloats, held);
-        store_held_wave(held, p.obs + ((size_t)f * p.n_total + wrow0) * DD_OBS_DIM, wfloats);
+        hold_obs_wave(tile[f & 1] + woff, held);
+        store_held_wave(held, rsrc_over(obs_prev, slice_bytes));
     }
     if (live) {
         store_spawn(reload_soa<RolloutArgs, T>(), i, s);  // every field: lanes may have re-spawned
@@ -959,6 +1012,13 @@ __global__ __launch_bounds__(kBlock) void compact_scatter_kernel(const uint8_t* 
     }
 }
 
+#ifdef DD_ISA_PROBE
+// tools/isa_probe.sh: one kernel instantiation alone (device assembly in
+// seconds instead of the whole library's minutes), for reading its ISA.
+#define DD_PROBE_KERNEL_(k) template __global__ void k;
+DD_PROBE_KERNEL_(DD_ISA_PROBE)
+}  // namespace dd
+#else
 // ---------------------------------------------------------------------------
 // Host side: argument checks, chunking and launches.
 // ---------------------------------------------------------------------------
@@ -1022,8 +1082,10 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
 
 template <typename T, int AFMT, bool kRef, bool kShaped>
 void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
-    // the held obs path needs every frame row start 16-byte aligned
-    const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0;
+    // the held obs path needs every frame row start 16-byte aligned, and
+    // (bitmask actions) a 4-byte aligned action buffer for its dword loads
+    const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0 &&
+                      (AFMT != DD_ACT_BITMASK || (reinterpret_cast<uintptr_t>(p.actions) & 3u) == 0);
     const unsigned blocks = (unsigned)tiles_of(p.n);
     if (held)
         hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true, kShaped>), dim3(blocks), dim3(kBlock),
@@ -1051,26 +1113,44 @@ void rollout_chunks(RolloutArgs p, const DDState& st, const DDRolloutIO& io, int
     p.act_stride = n * act_w;
     p.reward_stride = n * (int64_t)sizeof(T);
     p.n_total = n;
+    const int32_t frames = p.frames;
+    const int64_t step0 = p.action_step;
     for (int64_t first = 0; first < n; first += kChunk) {
         const int64_t len = n - first < kChunk ? n - first : kChunk;
-        p.actions = io.actions ? static_cast<const char*>(io.actions) + first * act_w : nullptr;
-        p.reward = reinterpret_cast<char*>(static_cast<T*>(io.reward) + first);
-        p.done = io.done + first;
-        p.obs = io.obs ? io.obs + first * DD_OBS_DIM : nullptr;
-        p.n = (int32_t)len;
-        const bool shaped = io.shaped_hist != nullptr;
-        p.shaped_hist = shaped ? io.shaped_hist + first : nullptr;
-        p.engine_reward = shaped && io.engine_reward
-                              ? reinterpret_cast<char*>(static_cast<T*>(io.engine_reward) + first) : nullptr;
-        p.engine_done = shaped && io.engine_reward ? io.engine_done + first : nullptr;
-        p.max_steps = io.max_steps;
-        const Soa<T> a = soa_of<T>(st, first);
-        if (ref) {
-            if (shaped) launch_rollout_fmt<T, true, true>(p, io.action_format, a, s);
-            else launch_rollout_fmt<T, true, false>(p, io.action_format, a, s);
-        } else {
-            if (shaped) launch_rollout_fmt<T, false, true>(p, io.action_format, a, s);
-            else launch_rollout_fmt<T, false, false>(p, io.action_format, a, s);
+        // The kernel reads actions by raw buffer loads with 32-bit offsets
+        // (buffer_action): a launch covers as many frames as keep every
+        // consumed offset, (frames - 1) x stride + len x width, below 2^32,
+        // and the state goes through memory between such launches (the same
+        // frames either way: the rollout equals its frames' dd_step calls).
+        int64_t fg = frames;
+        if (act_w > 0 && (fg - 1) * p.act_stride + len * act_w > (int64_t)UINT32_MAX)
+            fg = 1 + (((int64_t)UINT32_MAX - len * act_w) / p.act_stride);
+        for (int64_t g0 = 0; g0 < frames; g0 += fg) {
+            const int64_t ng = frames - g0 < fg ? frames - g0 : fg;
+            p.frames = (int32_t)ng;
+            p.action_step = step0 + g0;
+            p.actions = io.actions ? static_cast<const char*>(io.actions) + g0 * p.act_stride + first * act_w : nullptr;
+            // every byte the range check admits lies in the caller's buffer
+            const int64_t extent = (ng - 1) * p.act_stride + (n - first) * act_w;
+            p.act_bytes = (uint32_t)(extent < (int64_t)UINT32_MAX ? extent : (int64_t)UINT32_MAX);
+            p.reward = reinterpret_cast<char*>(static_cast<T*>(io.reward) + g0 * n + first);
+            p.done = io.done + g0 * n + first;
+            p.obs = io.obs ? io.obs + (g0 * n + first) * DD_OBS_DIM : nullptr;
+            p.n = (int32_t)len;
+            const bool shaped = io.shaped_hist != nullptr;
+            p.shaped_hist = shaped ? io.shaped_hist + first : nullptr;
+            p.engine_reward = shaped && io.engine_reward
+                                  ? reinterpret_cast<char*>(static_cast<T*>(io.engine_reward) + g0 * n + first) : nullptr;
+            p.engine_done = shaped && io.engine_reward ? io.engine_done + g0 * n + first : nullptr;
+            p.max_steps = io.max_steps;
+            const Soa<T> a = soa_of<T>(st, first);
+            if (ref) {
+                if (shaped) launch_rollout_fmt<T, true, true>(p, io.action_format, a, s);
+                else launch_rollout_fmt<T, true, false>(p, io.action_format, a, s);
+            } else {
+                if (shaped) launch_rollout_fmt<T, false, true>(p, io.action_format, a, s);
+                else launch_rollout_fmt<T, false, false>(p, io.action_format, a, s);
+            }
         }
     }
 }
@@ -1274,3 +1354,4 @@ int dd_lab_timeline(void* dst, int64_t bytes) {
 #endif
 
 }  // extern "C"
+#endif  // DD_ISA_PROBE

@@ -11,12 +11,12 @@ the CPU.
 from __future__ import annotations
 
 import os
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
-__all__ = ["shard_bounds", "dist_env", "gather_obs"]
+__all__ = ["shard_bounds", "dist_env", "gather_obs", "gather_state"]
 
 
 def shard_bounds(total: int, rank: int, world: int) -> Tuple[int, int]:
@@ -60,3 +60,26 @@ def gather_obs(obs: torch.Tensor, total: int, dst: int = 0, group=None) -> Optio
     if rank != dst:
         return None
     return torch.cat([g[:c] for g, c in zip(gathered, counts)], dim=0)
+
+
+def gather_state(fields: Dict[str, torch.Tensor], total: int, dst: int = 0, group=None) -> Optional[Dict[str, torch.Tensor]]:
+    """Gather per-drone tensors (each ``[count_r]`` or ``[count_r, k]``: the
+    SoA state fields, a frame's reward / done) from every rank to rank
+    ``dst`` as ``[total, ...]`` tensors in global env-id order (None on the
+    other ranks).  Fields of one dtype travel packed as the columns of one
+    block, so the exchange is one :func:`gather_obs` per dtype, not per
+    field: the consumer-side twin of the step path's shards (checkpoints,
+    a learner that needs the whole batch)."""
+    groups: Dict[torch.dtype, List[str]] = {}
+    for name, t in fields.items():
+        groups.setdefault(t.dtype, []).append(name)
+    out: Dict[str, torch.Tensor] = {}
+    for dtype, names in groups.items():
+        cols = [fields[n].reshape(fields[n].shape[0], -1) for n in names]
+        widths = [c.shape[1] for c in cols]
+        g = gather_obs(torch.cat(cols, dim=1), total, dst=dst, group=group)
+        if g is None:
+            continue
+        for n, piece in zip(names, torch.split(g, widths, dim=1)):
+            out[n] = piece.reshape((total,) + tuple(fields[n].shape[1:]))
+    return out if dist.get_rank(group) == dst else None

@@ -37,7 +37,28 @@ def test_cpu_baseline_fields():
     assert r["value"] == r["legs"]["python_objects"]["value"]
     assert r["legs"]["c_scalar"]["value"] > r["legs"]["python_objects"]["value"]  # C beats Python objects
     assert r["host_cores"] == os.cpu_count() and r["affinity_cores"] >= 1 and r["cpu_model"]
-    assert "16" in r["cores_note"]  # why workers != host_cores on the GPU pool
+    assert r["baseline_leg"] == "python_objects" and set(r["speedup_basis"]) == set(r["legs"])
+    sh = r["cpu_share"]
+    assert 1 <= sh["cores"] <= sh["affinity_cores"] and sh["source"]
+
+
+def test_cpu_share_from_cgroup_files(tmp_path):
+    # the worker count follows the cgroup quota when one is set
+    b = _bench()
+    proc = tmp_path / "cgroup"
+    proc.write_text("0::/job\n")
+    (tmp_path / "job").mkdir()
+    (tmp_path / "job" / "cpu.max").write_text("1600000 100000\n")
+    assert b._cgroup_quota(str(tmp_path), str(proc)) == (16.0, str(tmp_path / "job" / "cpu.max"))
+    (tmp_path / "job" / "cpu.max").write_text("max 100000\n")
+    q, why = b._cgroup_quota(str(tmp_path), str(proc))
+    assert q is None and "no CPU quota" in why
+    proc.write_text("4:cpu,cpuacct:/c1\n")  # cgroup v1
+    d = tmp_path / "cpu,cpuacct" / "c1"
+    d.mkdir(parents=True)
+    (d / "cpu.cfs_quota_us").write_text("800000\n")
+    (d / "cpu.cfs_period_us").write_text("100000\n")
+    assert b._cgroup_quota(str(tmp_path), str(proc))[0] == 8.0
 
 
 def test_pmc_traffic_only_for_the_measured_build(tmp_path):

@@ -15,6 +15,8 @@
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the step kernel at 262,144 and 16.8M drones
 #   sq         SQ instruction counters of the step / rollout kernels (tools/pmc_sq.sh)
 #   lab        tools/kernel_lab.py (VARIANTS, ENVS, LABARGS)
+#   roll       tools/rollout_lab.py (VARIANTS, ENVS, ROLLARGS e.g. --philox), appended to <tag>/roll.jsonl
+#   sqroll     SQ counters of dd_rollout per lab variant (tools/pmc_rollout_ab.sh; ROLLARGS, ROLLSUFFIX)
 #   mr         tools/multirank_check.py on 2 gloo ranks sharing GPU 0 (torchrun), output in <tag>/mr/
 #   py:<file>  python <file> (LABARGS passed through), output in <tag>/<file stem>.log
 set -o pipefail
@@ -61,6 +63,14 @@ run_step() {
     lab)
         timeout -k 10 600 python tools/kernel_lab.py --variants ${VARIANTS:-base} --envs ${ENVS:-262144,1048576,16777216} \
             ${LABARGS} > $OUT/lab.jsonl 2> $OUT/lab.err; local rc=$?; cat $OUT/lab.jsonl; tail -5 $OUT/lab.err; return $rc ;;
+    sqroll)
+        ( OUT2=$TAG/sqroll; LABARGS="${ROLLARGS}" TAGSUFFIX="${ROLLSUFFIX}" bash tools/pmc_rollout_ab.sh $OUT2 $(echo ${VARIANTS:-base} | tr , " ") ) ;;
+    roll)
+        timeout -k 10 600 python tools/rollout_lab.py --variants ${VARIANTS:-base} --envs ${ENVS:-65536,262144} \
+            ${ROLLARGS} >> $OUT/roll.jsonl 2>> $OUT/roll.err; local rc=$?; cat $OUT/roll.jsonl; tail -3 $OUT/roll.err; return $rc ;;
+    micro:*)
+        local m=${1#micro:}
+        timeout -k 10 300 tools/micro/$m > $OUT/$m.jsonl 2> $OUT/$m.err; local rc=$?; cat $OUT/$m.jsonl; return $rc ;;
     mr)
         timeout -k 10 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 \
             --master-port 29517 tools/multirank_check.py --backend gloo --out $OUT/mr > $OUT/mr.log 2>&1; local rc=$?

@@ -86,7 +86,7 @@ def main():
     import numpy as np
     import torch
     import torch.distributed as dist
-    from delivery_drone_amd.sharding import dist_env, gather_obs, shard_bounds
+    from delivery_drone_amd.sharding import dist_env, gather_obs, gather_state, shard_bounds
 
     rank, world, local = dist_env()
     ndev = torch.cuda.device_count()
@@ -106,17 +106,15 @@ def main():
     dt = time.perf_counter() - t0
     host = args.backend == "gloo"
 
-    def gathered(t):  # one [total, k] tensor on rank 0 (float32 / int32 payloads)
-        t = t.reshape(count, -1)
-        t = t.cpu() if host else t
-        return gather_obs(t, args.total, dst=0)
-
     t1 = time.perf_counter()
-    g_obs = gathered(o)
+    g_obs = gather_obs(o.cpu() if host else o, args.total, dst=0)
     gather_s = time.perf_counter() - t1
-    g_rew = gathered(r.to(torch.float32))
-    g_done = gathered(d.to(torch.int32))
-    g_state = {f: gathered(getattr(env, f).to(torch.float64 if f in FIELDS[:10] else torch.int32)) for f in FIELDS}
+    payload = {"reward": r.to(torch.float32), "done": d.to(torch.int32)}
+    payload.update({f: getattr(env, f).to(torch.float64 if f in FIELDS[:10] else torch.int32) for f in FIELDS})
+    g_all = gather_state({k: (v.cpu() if host else v) for k, v in payload.items()}, args.total, dst=0)
+    if rank == 0:
+        g_rew, g_done = g_all["reward"], g_all["done"]
+        g_state = {f: g_all[f] for f in FIELDS}
     if rank == 0:
         child = subprocess.run([sys.executable, os.path.abspath(__file__), "--single", "--total", str(args.total),
                                 "--frames", str(args.frames), "--seed", str(args.seed), "--out", args.out],

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box: SQ instruction / cycle counters of dd_rollout (65,536 x 256) for
 # each lab variant (tools/rollout_lab.py), one rocprofv3 pass per group.
-#   bash tools/pmc_rollout_ab.sh <outdir> <variant> [<variant> ...]
+#   [LABARGS=--philox] [TAGSUFFIX=_p] bash tools/pmc_rollout_ab.sh <outdir> <variant> [<variant> ...]
 set -o pipefail
 OUT=gpurun_out/${1:?out}
 shift
@@ -14,8 +14,8 @@ groups=(
 for v in "$@"; do
   i=0
   for g in "${groups[@]}"; do
-    timeout -s KILL 120 rocprofv3 --pmc $g --kernel-include-regex rollout_kernel -d $OUT/${v}_g$i -o pmc -f csv -- \
-      python3 tools/rollout_lab.py --variants $v --envs 65536 --rounds 2 > /dev/null 2>> $OUT/err.log \
+    timeout -s KILL 120 rocprofv3 --pmc $g --kernel-include-regex rollout_kernel -d $OUT/${v}${TAGSUFFIX}_g$i -o pmc -f csv -- \
+      python3 tools/rollout_lab.py --variants $v --envs 65536 --rounds 2 ${LABARGS} > /dev/null 2>> $OUT/err.log \
       || { echo "variant $v group $i failed"; exit 1; }
     i=$((i+1))
   done
