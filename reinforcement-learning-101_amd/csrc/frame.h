@@ -18,7 +18,7 @@
 
 // The reference's sin, cos and squares, bit for bit: libm_ref.h restates
 // glibc's (the reference calls np.sin / np.cos and `v ** 2` = glibc pow), with
-// their tables (tools/gen_libm_tables.py, from this image's libm) in device
+// their tables (csrc/libm_tables.h: glibc 2.35's, committed) in device
 // memory, for the rare frames near a predicate boundary (frame).
 #include "libm_tables.h"
 __device__ const double dd_libm_pow_tab[384] = DD_LIBM_POW_TAB;
@@ -400,8 +400,8 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     //   conversions the f32 store makes anyway);
     // * on the landing test's lanes (upright, within reach of the pad): the
     //   speed or the bottom centre within 2^-20 of its limit / a pad edge.
-    // y' = 650 never decides a flag (past 550 the drone has crashed or landed
-    // first); fuel, spin and angle involve no transcendental.
+    // Under kRef y' = 650 never decides a flag (past 550 the drone has crashed
+    // or landed first); fuel, spin and angle involve no transcendental.
     const auto close = [](double q, double b) { return fabs(q - b) <= 0x1p-20 * (1.0 + fabs(b)); };
     bool risky = false;
     if constexpr (!kExact) {
@@ -418,9 +418,12 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
             const float qx = fabsf(fabsf(xf - 400.0f) - 450.0f), qy = fabsf(fabsf(yf - 250.0f) - 300.0f);
             risky = fminf(qx, qy) == 0.0f;
         } else {
+            // (y' = world_height + margin too: with a ground level at or past
+            // that edge the out-of-bounds test can decide there)
             const bool q0 = close(s.y, c.ground_level), q1 = close(s.x, -c.oob_margin),
-                       q2 = close(s.x, c.world_width + c.oob_margin), q3 = close(s.y, -c.oob_margin);
-            risky = q0 | q1 | q2 | q3;
+                       q2 = close(s.x, c.world_width + c.oob_margin), q3 = close(s.y, -c.oob_margin),
+                       q4 = close(s.y, c.world_height + c.oob_margin);
+            risky = q0 | q1 | q2 | q3 | q4;
         }
     }
 

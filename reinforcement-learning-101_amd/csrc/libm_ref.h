@@ -1,4 +1,8 @@
 // libm_ref.h — the reference's transcendentals, bit for bit: glibc 2.35's
+// (License: this file restates GNU C Library code and is LGPL-2.1-or-later,
+// like its sources: e_pow.c (c) 2018 Arm Ltd., s_sin.c (c) IBM Corp.
+// 2001-2017 / the GNU C Library; see THIRD_PARTY_NOTICES.md.)
+//
 // pow(x, 2.0), sin and cos as the x86_64 library computes them (the FMA
 // builds its ifunc selects on any FMA-capable CPU, compiled with GCC's
 // default floating-point contraction), restated from glibc's published
@@ -31,7 +35,7 @@
 //   dd_libm_pow_tab[384]            {invc, logc, logctail} x 128   (DD_LIBM_POW_TAB)
 //   dd_libm_exp_tab[256]            {tail, sbits} x 128 as uint64  (DD_LIBM_EXP_TAB)
 //   dd_libm_sincos_tab[440]         {sn, ssn, cs, ccs} x 110       (DD_LIBM_SINCOS_TAB)
-// and includes libm_tables.h (tools/gen_libm_tables.py) for the scalar data.
+// and includes libm_tables.h (glibc 2.35's tables, committed; tools/gen_libm_tables.py) for the scalar data.
 #pragma once
 
 #include <stdint.h>

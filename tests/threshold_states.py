@@ -6,6 +6,8 @@ Families (each a share of the batch), the boundary and the variable moved:
 
   crash_y     y' = 550 (ground_level)                 y
   oob         x' = -50 / 850, y' = -50                x / y
+              (+ y' = world_height + margin = 650 when the config's
+              ground_level lies at or past it, where that edge decides)
   speed       speed' = 3 on the pad (landing test)     vx, vy (scaled)
   angle       |angle'| = 20 on the pad                 angle
   pad_x       bottom-centre x' = px -/+ 50, slow, upright   x
@@ -59,12 +61,17 @@ def _near_pad(rng, st, idx):
     st["y"][idx] = st["py"][idx] - 10 + rng.uniform(-8, 8, m)
 
 
-def generate(n: int, precision: str, seed: int = 0, iters: int = 6):
-    """(state dict, actions u8 [n], family index [n], target [n], which q column
-    [n]) with the targeted quantity within ~4 storage ulps of its boundary."""
+def generate(n: int, precision: str, seed: int = 0, iters: int = 6, config=None):
+    """(state dict, actions u8 [n], family index [n], distance in storage ulps
+    [n]) with the targeted quantity within ~4 storage ulps of its boundary,
+    under `config` (default config.py's; the boundaries follow its
+    ground_level, oob_margin and world size, and the oracle probe its wind)."""
     from oracle import oracle as ora
     from delivery_drone_amd import EnvConfig
 
+    cfg = config or EnvConfig()
+    ground, margin = float(cfg.ground_level), float(cfg.oob_margin)
+    top = float(cfg.world_height) + margin
     rng = np.random.default_rng(seed)
     st, acts = _base(rng, n)
     fam = rng.integers(0, len(FAMILIES), n)
@@ -75,19 +82,23 @@ def generate(n: int, precision: str, seed: int = 0, iters: int = 6):
         idx = np.flatnonzero(fam == f)
         m = idx.size
         if name == "crash_y":
-            col[idx], bound[idx], var[idx] = Q_Y, 550.0, "y"
+            col[idx], bound[idx], var[idx] = Q_Y, ground, "y"
+            g = int(ground)
             st["px"][idx] = rng.integers(100, 700, m)  # pads anywhere; some under the drone
-            st["py"][idx] = rng.integers(520, 560, m)
+            st["py"][idx] = rng.integers(g - 30, g + 10, m)
             st["x"][idx] = st["px"][idx] + rng.uniform(-80, 80, m)
+            st["y"][idx] = rng.uniform(g - 100, g + 90, m)
             st["vy"][idx] = rng.uniform(-1, 6, m)
             sel = rng.random(m) < 0.5  # half slow and upright: the on-pad crash tests
             _near_pad(rng, st, idx[sel])
-            st["py"][idx[sel]] = rng.integers(545, 556, int(sel.sum()))
+            st["py"][idx[sel]] = rng.integers(g - 5, g + 6, int(sel.sum()))
         elif name == "oob":
-            side = rng.integers(0, 3, m)
+            sides = 4 if ground >= top else 3  # the top edge decides only past the ground
+            side = rng.integers(0, sides, m)
             col[idx] = np.where(side < 2, Q_X, Q_Y)
-            bound[idx] = np.choose(side, [-50.0, 850.0, -50.0])
+            bound[idx] = np.choose(side, [-margin, float(cfg.world_width) + margin, -margin, top][:sides])
             var[idx] = np.where(side < 2, "x", "y")
+            st["y"][idx[side == 3]] = rng.uniform(top - 40, top + 40, int((side == 3).sum()))
         elif name == "speed":
             _near_pad(rng, st, idx)
             col[idx], bound[idx], var[idx] = Q_SPEED, 3.0, "speed"
@@ -112,7 +123,6 @@ def generate(n: int, precision: str, seed: int = 0, iters: int = 6):
     k = rng.integers(-4, 5, n)
     target = bound + k * _ulp(bound, precision)
     dt = np.float64 if precision == "f64" else np.float32
-    cfg = EnvConfig()
 
     def quantize():
         for f in ("x", "y", "vx", "vy", "angle", "omega", "fuel"):
