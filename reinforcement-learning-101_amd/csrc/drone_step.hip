@@ -355,7 +355,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
 }
 
 #ifdef DD_EXP_TIMELINE
-// Lab-only (tools/timeline_lab.py): per wave, the 100 MHz real-time clock at
+// Lab-only (tools/lab/timeline_lab.py): per wave, the 100 MHz real-time clock at
 // kernel entry, loads complete, frame done, obs issued and stores complete,
 // the shader-clock entry/exit, and HW_ID / XCC_ID, for the last launch.
 constexpr int kTlWaves = 1 << 14;

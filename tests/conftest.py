@@ -15,6 +15,29 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); parity tests through the C ABI")
 
 
+def pytest_sessionstart(session):
+    tr = session.config.pluginmanager.get_plugin("terminalreporter")
+    if tr is not None:  # also under -q, where pytest drops the report header
+        tr.write_line(_build_line())
+
+
+def _build_line():
+    """First lines of every run: the library under test, by the ABI version
+    and ISA hashes it reports (dd_build_info) and its file hash, so a GPU test
+    log names the build it tested (the bench line carries the same string)."""
+    import hashlib
+    lib = os.path.join(REPO, "reinforcement-learning-101_amd", "delivery_drone_amd", "_native", "libdronestep.so")
+    if not os.path.exists(lib):
+        return "libdronestep.so: not built yet (the session fixture builds it)"
+    try:
+        from delivery_drone_amd import abi
+        info = abi.lib().dd_build_info().decode()
+    except Exception as e:  # noqa: BLE001 - a header must not fail the run
+        info = f"(not loadable: {type(e).__name__}: {e})"
+    md5 = hashlib.md5(open(lib, "rb").read()).hexdigest()
+    return f"libdronestep.so build_info: {info}; md5={md5}"
+
+
 @pytest.fixture(scope="session", autouse=True)
 def _native_builds():
     """Build the oracle (gcc) and the product library.  On a GPU box (/dev/kfd

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Device assembly of drone_step.hip (+ extra -D flags) and the register /
 # spill metadata of the step and rollout kernels (no GPU needed).
-#   tools/isa_stats.sh [-DFLAG ...]   -> /tmp/isa/drone_step.s
+#   tools/lab/isa_stats.sh [-DFLAG ...]   -> /tmp/isa/drone_step.s
 set -e
-cd "$(dirname "$0")/../reinforcement-learning-101_amd"
+cd "$(dirname "$0")/../../reinforcement-learning-101_amd"
 mkdir -p /tmp/isa
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -I../include \
   --offload-device-only -S -o /tmp/isa/drone_step.s "$@" csrc/drone_step.hip 2>&1 | grep -v "unused during compilation" || true

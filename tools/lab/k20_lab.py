@@ -20,7 +20,7 @@ import statistics
 import sys
 import time
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
 
 _hip = ctypes.CDLL("libamdhip64.so")

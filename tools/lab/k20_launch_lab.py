@@ -5,7 +5,7 @@ settings that change only how the host submits work, and prints one JSON line
 per run with the wall and event times per step.  Lab tool: not part of the
 product or of the tests.
 
-    python tools/k20_launch_lab.py [--reps 3] [--steps 20]
+    python tools/lab/k20_launch_lab.py [--reps 3] [--steps 20]
 """
 import argparse
 import json
@@ -13,7 +13,7 @@ import os
 import subprocess
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 VARIANTS = {
     "base": ({}, []),

@@ -6,7 +6,7 @@ import os
 import statistics
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
 import torch  # noqa: E402
 from torch import nn  # noqa: E402

@@ -2,7 +2,7 @@
 """Lab: does the step's speed depend on where the SoA fields sit relative to
 each other?  Every variant is its own env; 'torch' keeps the caching
 allocator's placement, 'sS' carves all fields and outputs from one slab with
-field k at a 2 MiB boundary + k*S bytes (tools/diag_alloc.rebind_slab).
+field k at a 2 MiB boundary + k*S bytes (tools/lab/diag_alloc.rebind_slab).
 Timed in interleaved rounds (order reversed every other round).
 
 usage: placement_lab.py N variant [variant ...]   e.g. 16777216 torch s0 s4096
@@ -12,7 +12,7 @@ import os
 import statistics
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 import torch  # noqa: E402

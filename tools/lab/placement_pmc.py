@@ -5,14 +5,14 @@ env 2 x S, twice), so a rocprofv3 --pmc / --kernel-trace run of this script
 can attribute every step_kernel dispatch to its allocation by dispatch order.
 Prints one JSON line per env with its own event timing (median us/step).
 
-    rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum ... -- python3 tools/placement_pmc.py [S]
+    rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum ... -- python3 tools/lab/placement_pmc.py [S]
 """
 import json
 import os
 import statistics
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
 import torch  # noqa: E402
 

@@ -2,7 +2,7 @@
 """A/B timing of dd_policy_rollout builds (actor + sampling + frame per frame,
 one launch), interleaved ABBA rounds; prints us per frame per variant.
 
-    python tools/prl_lab.py --variants base,lnchain --envs 65536 --compute f16x3
+    python tools/lab/prl_lab.py --variants base,lnchain --envs 65536 --compute f16x3
 """
 import argparse
 import json
@@ -10,7 +10,7 @@ import os
 import statistics
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
 import torch  # noqa: E402
 from torch import nn  # noqa: E402

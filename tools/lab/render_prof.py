@@ -5,7 +5,7 @@ is its own trace record)."""
 import os
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
 import torch  # noqa: E402
 from delivery_drone_amd import EnvConfig, VecDroneEnv  # noqa: E402

@@ -7,7 +7,7 @@ have landed (t1), when the frame is done (t2), when its obs rows are issued
 prints, per variant and batch size, the phase percentiles relative to the
 first wave's entry and how the co-resident waves of one SIMD overlap.
 
-    python tools/timeline_lab.py --variants tl,tlnomath --envs 262144
+    python tools/lab/timeline_lab.py --variants tl,tlnomath --envs 262144
 """
 import argparse
 import ctypes
@@ -17,7 +17,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "reinforcement-learning-101_amd"))
 
 import torch  # noqa: E402
