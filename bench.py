@@ -484,6 +484,36 @@ def f64_point(n, seed, dev, steps=500, graph_steps=50):
             "kernel": "dd::step_kernel<double, 0, true, false>", "launch": f"hipGraph of {graph_steps} dd_step"}
 
 
+def ping_pong_point(n, seed, dev, steps=2000, graph_steps=50, rounds=3):
+    """The headline workload with VecDroneEnv(ping_pong=True) (DDStepIO.state_out:
+    the nine per-frame fields read from one copy and written to the other)
+    timed against in-place stepping of an identical env, interleaved rounds on
+    one box; the same bytes per env either way (each field is read once and
+    written once per step).  Graphs hold an even number of steps."""
+    import statistics
+    import torch
+    from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
+    envs = {m: VecDroneEnv(n, device=dev, config=cfg, ping_pong=(m == "ping_pong")) for m in ("in_place", "ping_pong")}
+    rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
+    ts = {m: [] for m in envs}
+    for e in envs.values():
+        e.reset()
+    for r in range(rounds):
+        for m in (list(envs) if r % 2 == 0 else list(envs)[::-1]):
+            ts[m].append(time_steps(envs[m], rows, steps, graph_steps, torch.cuda.Stream(dev)))
+    bpe = envs["in_place"].step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=True)
+    out = {"envs": n, "bytes_per_env": bpe, "launch": f"hipGraph of {graph_steps} dd_step", "rounds": rounds}
+    for m, t in ts.items():
+        ms = statistics.median(t)
+        gbs = bpe * n / (ms * 1e-3) / 1e9
+        out[m] = {"us_per_step": round(ms * 1e3, 3), "us_by_round": [round(x * 1e3, 3) for x in t],
+                  "steps_per_s": round(n / (ms * 1e-3), 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    del envs, rows
+    torch.cuda.empty_cache()
+    return out
+
+
 def gae_point(n, frames, dev):
     """dd_gae over a [frames, n] rollout: reads reward,
     value (+ bootstrap row), done; writes advantage and return."""
@@ -869,7 +899,7 @@ def main():
             gp = gather_point(env.obs, n, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
             gp = {"error": f"{type(e).__name__}: {e}"[:300]}
-    c5 = c5a = g5 = c2 = nb = f64p = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None
+    c5 = c5a = g5 = c2 = nb = f64p = ppp = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         c5a = step_loop_point(args.rollout_point, 256, args.precision, args.seed, dev)
@@ -878,6 +908,7 @@ def main():
         c2 = config2_point(args.seed, dev)
         nb = notebook_point(n, args.precision, args.seed, dev)
         f64p = f64_point(n, args.seed, dev)
+        ppp = ping_pong_point(n, args.seed, dev)
         pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
         pr = policy_rollout_point(args.rollout_point or 65_536, 64, args.seed, dev)
         pp16 = policy_point(args.rollout_point or 65_536, args.seed, dev, "f16x3")
@@ -942,6 +973,7 @@ def main():
             "gae_point": g5,
             "notebook_reward_point": nb,
             "f64_point": f64p,
+            "ping_pong_point": ppp,
             "policy_point": pp,
             "policy_rollout_point": pr,
             "policy_point_f16x3": pp16,

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 9  /* 9: packed MLP buffers carry a layout tag (dd_mlp_packed_floats + 4) */
+#define DD_ABI_VERSION 10 /* 10: DDStepIO.state_out (ping-pong state); 9: packed MLP buffers carry a layout tag */
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -178,6 +178,15 @@ typedef struct DDStepIO {
     uint8_t *shaped_done; /* uint8 [N]: done or truncated                        */
     int32_t max_steps;    /* <= 0: no truncation                                 */
     int32_t _pad2;
+    /* Ping-pong state (nullable = in place): the step reads the nine fields
+     * that change every frame (x y vx vy angle omega fuel total_reward steps)
+     * from `st` and writes them to *state_out's arrays, which must not alias
+     * st's; px, py, status and episode change only on a terminal frame or a
+     * re-spawn and stay in place (state_out's pointers for them must equal
+     * st's, and so must precision and env_id_base).  Separate in / out arrays
+     * spare the kernel the in-place update's end-of-launch write-back of lines
+     * it also read.  A sticky-done lane copies its fields. */
+    const struct DDState *state_out;
 } DDStepIO;
 
 /* Inputs and outputs of dd_rollout: `frames` consecutive frames, frame-major.

@@ -221,6 +221,7 @@ struct StepArgs {
     void* shaped_reward;
     uint8_t* shaped_done;
     int32_t max_steps;
+    int32_t ping_pong;     // DDStepIO.state_out set: the kernel's `o` is not `a`
 };
 
 #ifndef DD_STEP_MIN_WAVES
@@ -264,9 +265,12 @@ __device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, u
 // (LDS).  Returns whether the lane's episode ended in this call.  The fast
 // frame (kExact false) may report the lane risky (frame.h): then nothing is
 // stored, and the kernel calls finish_lane again with kExact.
+// `o`: where the nine per-frame fields go (x y vx vy angle omega fuel total
+// steps): `a` itself in place, the ping-pong arrays with DDStepIO.state_out
+// (px, py, status and episode always go to `a`).
 template <typename T, bool kRef, bool kShaped, bool kExact = false>
-__device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, uint32_t i, const Raw<T>& r,
-                                            float* orow, bool* risky = nullptr) {
+__device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, const Soa<T>& o, uint32_t i,
+                                            const Raw<T>& r, float* orow, bool* risky = nullptr) {
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     Lane s;
@@ -330,13 +334,14 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     // addresses, 22 VGPRs live across the frame).  A sticky-done lane
     // writes nothing; status and px only change on the terminal frame, a
     // respawn or a moving platform; py and episode only on a respawn.
-    const bool sticky = (r.status & DD_ST_DONE) && !respawned;
+    // (with separate out arrays a sticky lane copies its fields across)
+    const bool sticky = (r.status & DD_ST_DONE) && !respawned && !p.ping_pong;
     if (!sticky) {
         uint32_t j = i;
         asm volatile("" : "+v"(j));  // an offset defined in this block: isel folds it into saddr stores
-        store_dynamics(a, j, s);
-        put_state(a.steps, j, s.steps);
-        put_state(a.total, j, (T)s.total);
+        store_dynamics(o, j, s);
+        put_state(o.steps, j, s.steps);
+        put_state(o.total, j, (T)s.total);
         const bool moving = !kRef && sw.platform_moving;
         if (moving || respawned) put_state(a.px, j, (T)s.px);
         if (moving || ended || respawned) put_state(a.status, j, (uint8_t)s.status);
@@ -367,7 +372,7 @@ __device__ uint64_t dd_tl_buf[kTlWaves * 8];
 
 // dd_step kernel: one drone per lane, one tile of kStepBlock lanes per block.
 template <typename T, int AFMT, bool kRef, bool kShaped>
-__global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a) {
+__global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a, Soa<T> o) {
 #ifdef DD_EXP_EMPTY  // timing-only: the launch and dispatch floor
     if (p.n >= 0) return;
 #endif
@@ -384,6 +389,7 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
     // one scalar-load latency later than the state loads could start.
     asm volatile("" ::"s"(a.x), "s"(a.y), "s"(a.vx), "s"(a.vy), "s"(a.angle), "s"(a.omega), "s"(a.fuel),
                  "s"(a.px), "s"(a.py), "s"(a.total), "s"(a.status), "s"(a.steps), "s"(p.actions));
+    if (!p.ping_pong) o = a;  // in place: one set of store bases (SGPRs), as before ping-pong existed
     Raw<T> r;
     if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r);
 #ifdef DD_EXP_PAD_VALU  // timing-only: DD_EXP_PAD_VALU extra f64 FMAs per wave (4 chains), the VALU-cost slope
@@ -399,9 +405,10 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
     DD_TL(1);
 #endif
     bool risky = false;
-    bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM, &risky);
+    bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM,
+                                                                      &risky);
     if (__builtin_expect(__ballot(risky) != 0, 0)) {  // the rare exact pass (frame.h): glibc's sin, cos and pow
-        if (risky) ended = finish_lane<T, kRef, kShaped, true>(p, a, i, r, tile + threadIdx.x * DD_OBS_DIM);
+        if (risky) ended = finish_lane<T, kRef, kShaped, true>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM);
     }
     DD_TL(2);
     if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
@@ -598,6 +605,14 @@ __device__ __forceinline__ uint32_t buffer_action(__amdgpu_buffer_rsrc_t r, uint
 template <typename T, int AFMT, bool kRef, bool kHeld, bool kShaped>
 __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(RolloutArgs p, Soa<T> a) {
     __shared__ __attribute__((aligned(16))) float tile[kHeld ? 2 : 1][kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0)];
+#ifdef DD_EXP_S0_LDS
+    constexpr bool kParked = true;
+    __shared__ __attribute__((aligned(16))) LaneRecord<T> parked[kBlock];
+    LaneRecord<T>* const rec = &parked[threadIdx.x];
+#else
+    constexpr bool kParked = false;
+    LaneRecord<T>* const rec = nullptr;
+#endif
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     const uint32_t row0 = blockIdx.x * kBlock;
@@ -673,6 +688,7 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     asm volatile("" ::"v"(s.x), "v"(s.y), "v"(s.vx), "v"(s.vy), "v"(s.angle), "v"(s.omega), "v"(s.fuel),
                  "v"(s.px), "v"(s.py), "v"(s.total), "v"(s.status), "v"(s.steps), "v"(s.episode), "v"(act0),
                  "v"(act1));
+    if constexpr (kParked) quantize_park<T, false>(s, rec);  // frame 0's starting state (already quantized)
     // One frame; kObs and kAuto (auto_reset) are compile-time so the loop
     // body carries no uniform branch on them.
     auto run_frame = [&](const int f, uint32_t& slot, auto obs_c, auto auto_c) __attribute__((always_inline)) {
@@ -693,7 +709,10 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
         }
         double reward;
         const bool was_done = (s.status & DD_ST_DONE) != 0;
-        auto fast = [&]() __attribute__((always_inline)) { return frame_checked<kRef, true>(k, sw, act, s); };
+        auto fast = [&]() __attribute__((always_inline)) {
+            if constexpr (kParked) return frame_checked_parked<kRef, true, T>(k, sw, act, s, rec);
+            else return frame_checked<kRef, true>(k, sw, act, s);
+        };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
             // frame (a done lane's result is discarded), and a wave with a lane
@@ -747,7 +766,9 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
             put_out(done_p, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
         }
         if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
-        quantize<T, kRef>(s);  // the obs above sees the unrounded frame, like dd_step's
+        // the obs above sees the unrounded frame, like dd_step's
+        if constexpr (kParked) quantize_park<T, kRef>(s, rec);
+        else quantize<T, kRef>(s);
         if constexpr (kObs) {
             if constexpr (kHeld) {
                 store_held_wave(held, rsrc_over(obs_prev, prev_bytes));  // frame f - 1's rows
@@ -1036,18 +1057,18 @@ inline int64_t tiles_of(int64_t n) { return (n + kBlock - 1) / kBlock; }
 #endif
 
 template <typename T, int AFMT, bool kRef, bool kShaped>
-void launch_step(const StepArgs& p, const Soa<T>& a, hipStream_t s) {
+void launch_step(const StepArgs& p, const Soa<T>& a, const Soa<T>& o, hipStream_t s) {
     const unsigned blocks = (unsigned)((p.n + kStepBlock - 1) / kStepBlock);
     hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShaped>), dim3(blocks), dim3(kStepBlock), DD_EXP_STEP_DYN_LDS, s,
-                       p, a);
+                       p, a, o);
 }
 
 template <typename T, bool kRef, bool kShaped>
-void launch_step_fmt(const StepArgs& p, int afmt, const Soa<T>& a, hipStream_t s) {
+void launch_step_fmt(const StepArgs& p, int afmt, const Soa<T>& a, const Soa<T>& o, hipStream_t s) {
     switch (afmt) {
-        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK, kRef, kShaped>(p, a, s); break;
-        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3, kRef, kShaped>(p, a, s); break;
-        default: launch_step<T, DD_ACT_U8X3, kRef, kShaped>(p, a, s); break;
+        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK, kRef, kShaped>(p, a, o, s); break;
+        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3, kRef, kShaped>(p, a, o, s); break;
+        default: launch_step<T, DD_ACT_U8X3, kRef, kShaped>(p, a, o, s); break;
     }
 }
 
@@ -1070,12 +1091,14 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
         p.shaped_done = shaped ? io.shaped_done + first : nullptr;
         p.max_steps = io.max_steps;
         const Soa<T> a = soa_of<T>(st, first);
+        const Soa<T> o = io.state_out ? soa_of<T>(*io.state_out, first) : a;
+        p.ping_pong = io.state_out ? 1 : 0;
         if (ref) {
-            if (shaped) launch_step_fmt<T, true, true>(p, io.action_format, a, s);
-            else launch_step_fmt<T, true, false>(p, io.action_format, a, s);
+            if (shaped) launch_step_fmt<T, true, true>(p, io.action_format, a, o, s);
+            else launch_step_fmt<T, true, false>(p, io.action_format, a, o, s);
         } else {
-            if (shaped) launch_step_fmt<T, false, true>(p, io.action_format, a, s);
-            else launch_step_fmt<T, false, false>(p, io.action_format, a, s);
+            if (shaped) launch_step_fmt<T, false, true>(p, io.action_format, a, o, s);
+            else launch_step_fmt<T, false, false>(p, io.action_format, a, o, s);
         }
     }
 }
@@ -1179,6 +1202,17 @@ int dd_step(const DDConfig* cfg, const DDState* st, const DDStepIO* io, int64_t 
     }
     if (n == 0) return 0;  // empty batch: pointers may be null
     if (!dd::state_ok(st) || !io->actions || !io->reward || !io->done) return hipErrorInvalidValue;
+    if (const DDState* so = io->state_out) {  // ping-pong: the shared fields, distinct per-frame arrays
+        if (!dd::state_ok(so) || so->precision != st->precision || so->env_id_base != st->env_id_base ||
+            so->px != st->px || so->py != st->py || so->status != st->status || so->episode != st->episode)
+            return hipErrorInvalidValue;
+        const void* in[9] = {st->x, st->y, st->vx, st->vy, st->angle, st->omega, st->fuel, st->total_reward,
+                             st->steps};
+        const void* out[9] = {so->x, so->y, so->vx, so->vy, so->angle, so->omega, so->fuel, so->total_reward,
+                              so->steps};
+        for (int q = 0; q < 9; ++q)
+            if (in[q] == out[q]) return hipErrorInvalidValue;
+    }
     dd::StepArgs p{};
     p.k = dd::make_consts(*cfg);
     p.done_idx = io->done_idx;

@@ -593,6 +593,85 @@ __device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig&
     return reward;
 }
 
+// The state a frame starts from, parked in LDS (one record per lane) for the
+// rare exact redo of a rollout loop, instead of a register copy of the Lane
+// that stays live across the whole fast frame (frame_checked's s0: 27 VGPRs
+// at the kernel's register limit).  Written by quantize_park at the end of
+// every frame (the storage-width values quantize makes anyway, so no extra
+// conversion) and once before the first; read back only by a risky lane.
+// Storage width T: float records are 16 dwords, double records 24, both as
+// 16-byte LDS writes.
+template <typename T>
+struct LaneRecord {
+    uint32_t w[sizeof(T) == 4 ? 16 : 24];
+};
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ void park_lane(LaneRecord<T>* rec, const T v[10], uint32_t status, int32_t steps,
+                                          int32_t episode) {
+    uint32_t w[sizeof(T) == 4 ? 16 : 24];
+    memcpy(w, v, 10 * sizeof(T));
+    constexpr int o = 10 * sizeof(T) / 4;
+    w[o] = status;
+    w[o + 1] = (uint32_t)steps;
+    w[o + 2] = (uint32_t)episode;
+#pragma unroll
+    for (int q = o + 3; q < (int)(sizeof(w) / 4); ++q) w[q] = 0u;
+    u32x4_t* d = reinterpret_cast<u32x4_t*>(rec->w);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(w) / 16); ++q) d[q] = u32x4_t{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+}
+
+template <typename T>
+__device__ __forceinline__ void unpark_lane(const LaneRecord<T>* rec, Lane& s) {
+    uint32_t w[sizeof(T) == 4 ? 16 : 24];
+    const u32x4_t* d = reinterpret_cast<const u32x4_t*>(rec->w);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(w) / 16); ++q) {
+        const u32x4_t x = d[q];
+        w[4 * q] = x[0]; w[4 * q + 1] = x[1]; w[4 * q + 2] = x[2]; w[4 * q + 3] = x[3];
+    }
+    T v[10];
+    memcpy(v, w, 10 * sizeof(T));
+    constexpr int o = 10 * sizeof(T) / 4;
+    s.x = v[0]; s.y = v[1]; s.vx = v[2]; s.vy = v[3]; s.angle = v[4]; s.omega = v[5]; s.fuel = v[6];
+    s.px = v[7]; s.py = v[8]; s.total = v[9];
+    s.status = w[o];
+    s.steps = (int32_t)w[o + 1];
+    s.episode = (int32_t)w[o + 2];
+    s.speed = 0.0;  // (frame() measures the state it produces)
+    s.dist = 0.0;
+}
+
+// quantize (below) and park the result: the next frame's starting state.
+template <typename T, bool kRef = false>
+__device__ __forceinline__ void quantize_park(Lane& s, LaneRecord<T>* rec) {
+    const T v[10] = {(T)s.x, (T)s.y, (T)s.vx, (T)s.vy, (T)s.angle, (T)s.omega, (T)s.fuel, (T)s.px, (T)s.py,
+                     (T)s.total};
+    s.x = v[0]; s.y = v[1]; s.vx = v[2]; s.vy = v[3]; s.angle = v[4]; s.omega = v[5]; s.fuel = v[6];
+    s.total = v[9];
+    if constexpr (!kRef) { s.px = v[7]; s.py = v[8]; }
+    park_lane<T>(rec, v, s.status, s.steps, s.episode);
+}
+
+// frame_checked with the starting state in `rec` (parked) rather than in
+// registers: the fast frame, and for a risky lane the exact frame from the
+// parked state (a wave-uniform rare branch).
+template <bool kRef, bool kFlat, typename T>
+__device__ __forceinline__ double frame_checked_parked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s,
+                                                       const LaneRecord<T>* rec) {
+    bool risky = false;
+    double reward = frame<kRef, kFlat>(k, sw, act, s, &risky);
+    if (__builtin_expect(__ballot(risky) != 0, 0)) {
+        if (risky) {
+            unpark_lane<T>(rec, s);
+            reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
+        }
+    }
+    return reward;
+}
+
 // DroneGame.get_state (game_engine.py:140-177) in state_to_array order, as
 // doubles (columns 0-12; 13/14 are the landed / crashed flags); measure() has
 // run on `s`.  kExactDiv: the reference's quotients bit for bit (x / d by

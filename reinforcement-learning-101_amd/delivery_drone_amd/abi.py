@@ -20,7 +20,7 @@ __all__ = [
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 9
+DD_ABI_VERSION = 10
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
@@ -79,7 +79,7 @@ class DDStepIO(ctypes.Structure):
         ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("obs", ctypes.c_void_p),
         ("done_idx", ctypes.c_void_p), ("done_count", ctypes.c_void_p),
         ("shaped_hist", ctypes.c_void_p), ("shaped_reward", ctypes.c_void_p), ("shaped_done", ctypes.c_void_p),
-        ("max_steps", _I), ("_pad2", _I),
+        ("max_steps", _I), ("_pad2", _I), ("state_out", ctypes.c_void_p),
     ]
 
 

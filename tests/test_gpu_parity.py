@@ -10,6 +10,7 @@ Tolerances:
 * f32 storage: the same double result rounded once to float32, so within
   1 float32 ulp of the reference (2 allowed) and flags exact.
 """
+import ctypes
 import numpy as np
 import pytest
 import torch
@@ -492,3 +493,61 @@ def test_notebook_mode_matches_oracle_over_episodes(gpu_device):
         timeouts += int(((host(env.steps) == 300) & host(sdone)).sum())
     assert worst < 1e-9
     assert timeouts > 0  # some episodes hit the 300-step cap
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("auto", [True, False])
+def test_ping_pong_equals_in_place(precision, auto, gpu_device):
+    """VecDroneEnv(ping_pong=True) (DDStepIO.state_out: read one copy of the
+    per-frame fields, write the other) gives the in-place step's bits: every
+    output and every field, sticky-done lanes (which must copy their fields
+    across) and re-spawns included, and replayed hipGraphs of an even number
+    of steps."""
+    n, k = 10_007, 120
+    cfg = dict(randomize_drone=True, auto_reset=auto, seed=21)
+    a = VecDroneEnv(n, device=gpu_device, precision=precision, **cfg)
+    b = VecDroneEnv(n, device=gpu_device, precision=precision, ping_pong=True, **cfg)
+    a.reset()
+    b.reset()
+    g = torch.Generator(device=gpu_device).manual_seed(4)
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8, generator=g)
+    for t in range(k):
+        oa, ra, da, _ = a.step(acts[t])
+        ob, rb, db, _ = b.step(acts[t])
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    for f in gd.FLOAT_FIELDS + ("status", "steps", "episode"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert (a.status & gd.ST_DONE).any()  # done lanes were stepped (sticky or re-spawned)
+    # a graph of an even number of steps replays from the copy it ends on
+    s = torch.cuda.Stream(gpu_device)
+    s.wait_stream(torch.cuda.current_stream(gpu_device))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        for t in range(4):
+            b.step(acts[t])
+    for _ in range(3):
+        graph.replay()
+        for t in range(4):
+            a.step(acts[t])
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b.obs)
+    for f in gd.FLOAT_FIELDS + ("status", "steps", "episode"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_ping_pong_rejects_aliasing_and_lane_slices(gpu_device):
+    from delivery_drone_amd import abi
+    env = VecDroneEnv(256, device=gpu_device, ping_pong=True)
+    env.reset()
+    with pytest.raises(ValueError):
+        env.step(torch.zeros(128, dtype=torch.uint8, device=gpu_device), lanes=slice(0, 128))
+    io = abi.DDStepIO()
+    acts = torch.zeros(256, dtype=torch.uint8, device=gpu_device)
+    io.actions, io.reward, io.done = acts.data_ptr(), env.reward.data_ptr(), env._done.data_ptr()
+    io.state_out = ctypes.cast(ctypes.pointer(env._state), ctypes.c_void_p)  # out aliases in
+    stream = torch.cuda.current_stream(gpu_device).cuda_stream
+    assert env._lib.dd_step(ctypes.byref(env._cfg), ctypes.byref(env._state), ctypes.byref(io), 256, stream) != 0
+    bad = env._make_state(env._twin)
+    bad.px = env._twin["x"].data_ptr()  # a shared field that differs
+    io.state_out = ctypes.cast(ctypes.pointer(bad), ctypes.c_void_p)
+    assert env._lib.dd_step(ctypes.byref(env._cfg), ctypes.byref(env._state), ctypes.byref(io), 256, stream) != 0
