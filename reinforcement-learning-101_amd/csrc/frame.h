@@ -343,6 +343,22 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         thrust(sa, ca, &dvx, &dvy);
         s.vx = main_on ? s.vx + dvx : s.vx;
         s.vy = main_on ? s.vy + dvy : s.vy;
+#ifdef DD_EXP_SEL
+      if constexpr (kRef) {
+        // (config.py's finite constants) the gated fuel and spin terms as a
+        // selected operand instead of a selected result: x - 0.0 and
+        // x + (-0.0) are x for every x (signed zeros included), and a
+        // selected term gives the reference's one rounding (fma with a factor
+        // of 1.0 is the plain sum); each select is one v_cndmask on a high
+        // word (the low words are zero)
+        s.fuel = s.fuel - (main_on ? c.fuel_main : 0.0);
+        const bool left_on = (act & 2u) && s.fuel > 0.0;
+        s.omega = fma(-c.side_thrust_power, left_on ? 1.0 : 0.0, s.omega);
+        s.fuel = s.fuel - (left_on ? c.fuel_side : 0.0);
+        const bool right_on = (act & 4u) && s.fuel > 0.0;
+        s.omega = fma(c.side_thrust_power, right_on ? 1.0 : -0.0, s.omega);
+        s.fuel = s.fuel - (right_on ? c.fuel_side : 0.0);
+      } else {
         s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
         const bool left_on = (act & 2u) && s.fuel > 0.0;
         s.omega = left_on ? s.omega - c.side_thrust_power : s.omega;
@@ -350,6 +366,16 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         const bool right_on = (act & 4u) && s.fuel > 0.0;
         s.omega = right_on ? s.omega + c.side_thrust_power : s.omega;
         s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
+      }
+#else
+        s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
+        const bool left_on = (act & 2u) && s.fuel > 0.0;
+        s.omega = left_on ? s.omega - c.side_thrust_power : s.omega;
+        s.fuel = left_on ? s.fuel - c.fuel_side : s.fuel;
+        const bool right_on = (act & 4u) && s.fuel > 0.0;
+        s.omega = right_on ? s.omega + c.side_thrust_power : s.omega;
+        s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
+#endif
     } else {
         if (main_on) {
             double sa, ca, dvx, dvy;
@@ -433,7 +459,16 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     const double rx = c.platform_half_width + fabs(c.drone_half_height);
     const double ry = c.platform_half_height + fabs(c.drone_half_height);
     const double slack = 1.0 + 1e-9 * (fabs(s.x) + fabs(s.y) + fabs(s.px) + fabs(s.py) + rx + ry);
-    if (upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack) {
+#ifdef DD_EXP_FLAT_NEAR
+    // kFlat: the three tests as one predicate (bitwise &: no short-circuit),
+    // so the rare body sits behind one exec-mask branch instead of three
+    // nested ones that most waves enter (upright lanes are common)
+    const bool near_pad = kFlat ? (upright & (fabs(s.x - s.px) <= rx + slack) & (fabs(s.y - s.py) <= ry + slack))
+                                : (upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack);
+#else
+    const bool near_pad = upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack;
+#endif
+    if (near_pad) {
         // (lanes out of this reach of the pad: on_pad = false exactly as the
         // reference's comparisons give, the bottom centre lying within
         // |half_height| (+ rounding) of (x, y); NaN fails both tests alike)
