@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -596,15 +597,143 @@ __device__ __forceinline__ uint32_t buffer_action(__amdgpu_buffer_rsrc_t r, uint
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split rollout (kSplit: kRef, unshaped, held obs, one block per CU).  A block
+// is 8 waves: waves 0-3 step the drones (the "frame" waves), waves 4-7 write
+// the frames' outputs (the "writer" waves), one writer per frame wave, which
+// the dispatcher places on the same SIMD (wave w and w + 4 of a block).  At
+// 65,536 drones the single-role kernel runs one wave per SIMD, which issues
+// about one instruction per 2.5 ns — half the SIMD's rate; the writer's
+// instructions (the observation's 13 quotients and conversions, the row
+// staging, every output store and its waits) go into the other half.  A
+// frame wave hands each frame over through LDS as 6 (float) or 7 (double)
+// float4 per lane: the unrounded doubles the observation reads, the status
+// and the reward as stored.
+// Hand-over: two slots per pair, two counters in LDS.  produced[w] = frames
+// the frame wave has written, consumed[w] = frames the writer has finished
+// with.  LDS executes one wave's operations in issue order, so a counter
+// written after the data (program order, a compiler barrier between) is seen
+// only after the data is; no s_waitcnt is needed on either side.  The frame
+// wave writes slot f & 1 once consumed >= f - 1 (the writer is done with
+// frame f - 2; it reads that counter at the frame's start, so the wait at
+// the end is normally already satisfied).  Deadlock-free: the writer only
+// waits for frames the frame wave has produced, the frame wave only for the
+// writer to finish frames it has produced.
+// Every wait is bounded (kSpinCap polls of ~64 clocks, ~30 ms): a broken
+// hand-over ends the kernel with wrong rows, never a wave that spins forever.
+constexpr int kSpinCap = 1 << 20;
+template <typename T>
+constexpr int kStageQ = std::is_same<T, double>::value ? 7 : 6;
+
+struct D2 {
+    double a, b;
+};
+__device__ __forceinline__ f32x4 pack2(double a, double b) { return __builtin_bit_cast(f32x4, D2{a, b}); }
+__device__ __forceinline__ D2 unpack2(f32x4 v) { return __builtin_bit_cast(D2, v); }
+
+// (the value is a VGPR: readfirstlane it where it is tested, so a read issued
+// early does not wait for the LDS at the read)
+__device__ __forceinline__ int ctr_load(const int* c) {
+    return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ctr_store(int* c, int v) {
+    asm volatile("" ::: "memory");  // after every LDS access before it in program order
+    __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// slot: this wave's kStageQ x 64 float4 of one frame (float4 q of lane l at q * 64 + l)
+template <typename T>
+__device__ __forceinline__ void stage_put(f32x4* slot, uint32_t lane, const Lane& s, T reward) {
+    slot[0 * kWave + lane] = pack2(s.x, s.y);
+    slot[1 * kWave + lane] = pack2(s.vx, s.vy);
+    slot[2 * kWave + lane] = pack2(s.angle, s.omega);
+    slot[3 * kWave + lane] = pack2(s.fuel, s.px);
+    slot[4 * kWave + lane] = pack2(s.py, s.dist);
+    f32x4 q5 = pack2(s.speed, 0.0);
+    q5[2] = __builtin_bit_cast(float, s.status);
+    if constexpr (std::is_same<T, float>::value) q5[3] = reward;
+    slot[5 * kWave + lane] = q5;
+    if constexpr (std::is_same<T, double>::value) slot[6 * kWave + lane] = pack2(reward, 0.0);
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_get(const f32x4* slot, uint32_t lane, Lane& s, T& reward) {
+    f32x4 q[kStageQ<T>];
+#pragma unroll
+    for (int j = 0; j < kStageQ<T>; ++j) q[j] = slot[j * kWave + lane];
+    D2 d = unpack2(q[0]);
+    s.x = d.a, s.y = d.b;
+    d = unpack2(q[1]);
+    s.vx = d.a, s.vy = d.b;
+    d = unpack2(q[2]);
+    s.angle = d.a, s.omega = d.b;
+    d = unpack2(q[3]);
+    s.fuel = d.a, s.px = d.b;
+    d = unpack2(q[4]);
+    s.py = d.a, s.dist = d.b;
+    s.speed = unpack2(q[5]).a;
+    s.status = __builtin_bit_cast(uint32_t, q[5][2]);
+    if constexpr (std::is_same<T, float>::value) reward = q[5][3];
+    else reward = unpack2(q[6]).a;
+}
+
 #ifndef DD_ROLL_MIN_WAVES
 // per SIMD: 2 keeps the kernel within 256 registers in all (1 let the Philox-action
 // variant take 2 AGPRs on top of 256 VGPRs, one wave per SIMD at 262,144 drones:
 // +38 %); 4 caps it at 128 VGPRs and spills (A/B: DESIGN.md section 4)
 #define DD_ROLL_MIN_WAVES 2
 #endif
-template <typename T, int AFMT, bool kRef, bool kHeld, bool kShaped>
-__global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(RolloutArgs p, Soa<T> a) {
-    __shared__ __attribute__((aligned(16))) float tile[kHeld ? 2 : 1][kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0)];
+template <typename T, int AFMT, bool kRef, bool kHeld, bool kShaped, bool kSplit = false>
+__global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(RolloutArgs p,
+                                                                                                  Soa<T> a) {
+    static_assert(!kSplit || (kRef && kHeld && !kShaped), "the split rollout covers the reference config's held path");
+    // kSplit: the frame hand-over slots (the writer stages its rows in the
+    // slot it has just read); otherwise the observation tile
+    constexpr int kTileFloats = kSplit ? 4 : kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0);
+    __shared__ __attribute__((aligned(16))) float tile[kHeld && !kSplit ? 2 : 1][kTileFloats];
+    __shared__ __attribute__((aligned(16))) f32x4 stage[kSplit ? kBlock / kWave : 1][2][kSplit ? kStageQ<T> : 1]
+                                                      [kSplit ? kWave : 1];
+    __shared__ int ctr[2][kBlock / kWave];  // kSplit: produced, consumed
+    if constexpr (kSplit) {
+        if (threadIdx.x < 2 * (kBlock / kWave)) ctr[threadIdx.x >> 2][threadIdx.x & 3] = 0;
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= kBlock) {  // a writer wave
+            const uint32_t ht = threadIdx.x - kBlock, lane = ht & (kWave - 1);
+            const uint32_t wv = __builtin_amdgcn_readfirstlane(ht / kWave);  // uniform: SGPR store bases
+            const uint32_t hrow0 = blockIdx.x * kBlock;
+            const uint32_t hi = hrow0 + ht < (uint32_t)p.n ? hrow0 + ht : (uint32_t)p.n - 1;  // shadows, as below
+            const uint32_t hw0 = hrow0 + wv * kWave;
+            const int hrows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - hw0));
+            const uint32_t hslice = (uint32_t)hrows * (DD_OBS_DIM * 4);
+            char* rew_p = p.reward;
+            uint8_t* done_p = p.done;
+            const float* obs_f = p.obs + (int64_t)hw0 * DD_OBS_DIM;
+            for (int f = 0; f < p.frames; ++f) {
+                for (int spin = 0; __builtin_amdgcn_readfirstlane(ctr_load(&ctr[0][wv])) <= f && spin < kSpinCap; ++spin)
+                    __builtin_amdgcn_s_sleep(1);
+                asm volatile("" ::: "memory");
+                f32x4* slot = &stage[wv][f & 1][0][0];
+                Lane s;
+                T reward;
+                stage_get<T>(slot, lane, s, reward);
+                asm volatile("" ::: "memory");  // every lane's reads issue before any row write
+                put_out(reinterpret_cast<T*>(rew_p), hi, reward);
+                put_out(done_p, hi, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
+                // the rows go where the slot's data was (read above, in order)
+                float* rows = reinterpret_cast<float*>(slot);
+                observe<false>(kRefConsts, s, rows + lane * DD_OBS_DIM);
+                __syncwarp();
+                HeldObs h;
+                hold_obs_wave(rows, h);
+                ctr_store(&ctr[1][wv], f + 1);  // after the reads of the slot
+                store_held_wave(h, rsrc_over(obs_f, hslice));
+                obs_f += p.n_total * DD_OBS_DIM;
+                rew_p += p.reward_stride;
+                done_p += p.n_total;
+            }
+            return;
+        }
+    }
 #ifdef DD_EXP_S0_LDS
     constexpr bool kParked = true;
     __shared__ __attribute__((aligned(16))) LaneRecord<T> parked[kBlock];
@@ -693,7 +822,10 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     // body carries no uniform branch on them.
     auto run_frame = [&](const int f, uint32_t& slot, auto obs_c, auto auto_c) __attribute__((always_inline)) {
         constexpr bool kObs = decltype(obs_c)::value, kAuto = decltype(auto_c)::value;
-        if (kHeld && kObs) {
+        int consumed = 0;
+        if constexpr (kSplit) {
+            consumed = ctr_load(&ctr[1][threadIdx.x / kWave]);  // used at the hand-over, at the frame's end
+        } else if (kHeld && kObs) {
             __syncwarp();  // frame f - 1's rows (other lanes of this wave) are in LDS
             hold_obs_wave(tile[(f - 1) & 1] + woff, held);
         }
@@ -761,15 +893,26 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
                 put_out(reinterpret_cast<T*>(erew_p), i, (T)reward);
                 put_out(edone_p, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
             }
+        } else if constexpr (kSplit) {
+            // hand frame f to the writer (the unrounded frame, as the obs below)
+            const int wv = threadIdx.x / kWave;
+            // slot f & 1 still holds frame f - 2
+            for (int spin = 0; __builtin_amdgcn_readfirstlane(consumed) < f - 1 && spin < kSpinCap; ++spin) {
+                __builtin_amdgcn_s_sleep(1);
+                consumed = ctr_load(&ctr[1][wv]);
+            }
+            asm volatile("" ::: "memory");
+            stage_put<T>(&stage[wv][f & 1][0][0], threadIdx.x & (kWave - 1), s, (T)reward);
+            ctr_store(&ctr[0][wv], f + 1);
         } else {
             put_out(reinterpret_cast<T*>(rew_p), i, (T)reward);
             put_out(done_p, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
         }
-        if constexpr (kObs) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
+        if constexpr (kObs && !kSplit) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
         // the obs above sees the unrounded frame, like dd_step's
         if constexpr (kParked) quantize_park<T, kRef>(s, rec);
         else quantize<T, kRef>(s);
-        if constexpr (kObs) {
+        if constexpr (kObs && !kSplit) {
             if constexpr (kHeld) {
                 store_held_wave(held, rsrc_over(obs_prev, prev_bytes));  // frame f - 1's rows
                 prev_bytes = slice_bytes;
@@ -798,14 +941,14 @@ __global__ __launch_bounds__(kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(Roll
     };
     using yes = std::true_type;
     using no = std::false_type;
-    if (p.obs) {
+    if (kSplit || p.obs) {  // (kSplit: launched with obs; the writers wait for every frame)
         if (sw.auto_reset) run(yes{}, yes{});
         else run(yes{}, no{});
     } else {
         if (sw.auto_reset) run(no{}, yes{});
         else run(no{}, no{});
     }
-    if (kHeld && p.obs && p.frames > 0) {  // the last frame's slice
+    if (!kSplit && kHeld && p.obs && p.frames > 0) {  // the last frame's slice
         const int f = p.frames - 1;
         __syncwarp();
         hold_obs_wave(tile[f & 1] + woff, held);
@@ -1103,6 +1246,25 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
     }
 }
 
+// The split rollout (rollout_kernel's kSplit) when the launch is one block per
+// CU or fewer: its block takes 8 waves of ~256 registers, all of a CU's
+// register file for 256 drones, where the single-role kernel fits two blocks
+// (262,144 drones: 4 rounds of split blocks against 2 of single-role ones).
+// DD_ROLL_SPLIT=0 in the environment (read once) keeps the single-role kernel.
+inline bool split_rollout_fits(unsigned blocks) {
+    static const bool enabled = [] {
+        const char* e = getenv("DD_ROLL_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    if (!enabled) return false;
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    if (cus[dev] == 0 && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    return blocks <= (unsigned)cus[dev];
+}
+
 template <typename T, int AFMT, bool kRef, bool kShaped>
 void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
     // the held obs path needs every frame row start 16-byte aligned, and
@@ -1110,6 +1272,13 @@ void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
     const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0 &&
                       (AFMT != DD_ACT_BITMASK || (reinterpret_cast<uintptr_t>(p.actions) & 3u) == 0);
     const unsigned blocks = (unsigned)tiles_of(p.n);
+    if constexpr (kRef && !kShaped) {
+        if (held && p.obs && split_rollout_fits(blocks)) {
+            hipLaunchKernelGGL((rollout_kernel<T, AFMT, true, true, false, true>), dim3(blocks), dim3(2 * kBlock),
+                               DD_EXP_ROLL_DYN_LDS, s, p, a);
+            return;
+        }
+    }
     if (held)
         hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true, kShaped>), dim3(blocks), dim3(kBlock),
                            DD_EXP_ROLL_DYN_LDS, s, p, a);
