@@ -213,6 +213,25 @@ def test_rollout_large_ragged_equals_step_loop(gpu_device):
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("auto", [True, False])
+def test_split_rollout_full_chip_equals_step_loop(precision, auto, gpu_device):
+    """One block per CU (the split kernel's frame / writer waves: 65,532 lanes,
+    the last wave 60 rows), an odd frame count, both done modes."""
+    n, k = 65_532, 9
+    roll, loop = twins(n, gpu_device, precision, randomize_drone=True, auto_reset=auto, seed=21)
+    warm = torch.randint(0, 8, (150, n), device=gpu_device, dtype=torch.uint8)
+    roll.rollout(warm)  # mid-episode lanes, some done
+    loop.rollout(warm)
+    assert_same_state(roll, loop)
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
+    obs, reward, done = roll.rollout(acts)
+    for t in range(k):
+        o, r, d, _ = loop.step(acts[t])
+        assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
+    assert_same_state(roll, loop)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("n", [777, 4100])
 @pytest.mark.parametrize("cfg", [dict(platform_moving=True), dict(wind_enabled=True, wind_x=0.05, wind_y=-0.02),
                                  dict(auto_reset=False), dict(gravity=0.31, auto_reset=True)])

@@ -23,6 +23,10 @@ fi
 for v in ${VARIANTS:-base}; do
   case $v in
     base) build base ;;
+    flat) build flat -DDD_EXP_FLAT_NEAR ;;
+    s0lds) build s0lds -DDD_EXP_S0_LDS ;;
+    flats0) build flats0 -DDD_EXP_FLAT_NEAR -DDD_EXP_S0_LDS ;;
+    sel) build sel -DDD_EXP_SEL ;;
     ocml) build ocml -DDD_TRIG_OCML ;;
     plainobs) build plainobs -DDD_ST_OBS=0 ;;
     nofma) build nofma -DDD_TRIG_NO_FMA ;;

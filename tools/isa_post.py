@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Device-assembly post-pass for gfx950 (the product build runs it on the
-step / rollout kernels' .s before assembling them).
+"""Device-assembly post-pass for gfx950 (lab builds only, tools/build_post.sh:
+the step / rollout kernels' .s rewritten before assembling them; measured and
+dropped).
 
     python3 tools/isa_post.py IN.s OUT.s
 
