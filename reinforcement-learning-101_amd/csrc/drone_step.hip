@@ -628,8 +628,6 @@ constexpr int kStageQ = std::is_same<T, double>::value ? 7 : 6;
 struct D2 {
     double a, b;
 };
-__device__ __forceinline__ f32x4 pack2(double a, double b) { return __builtin_bit_cast(f32x4, D2{a, b}); }
-__device__ __forceinline__ D2 unpack2(f32x4 v) { return __builtin_bit_cast(D2, v); }
 
 // (the value is a VGPR: readfirstlane it where it is tested, so a read issued
 // early does not wait for the LDS at the read)
@@ -641,26 +639,46 @@ __device__ __forceinline__ void ctr_store(int* c, int v) {
     __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// slot: this wave's kStageQ x 64 float4 of one frame (float4 q of lane l at q * 64 + l)
+// slot: this wave's kStageQ x 64 float4 of one frame (float4 q of lane l at q * 64 + l).
+// Never __builtin_bit_cast a vector ELEMENT (v[i], v.x): ROCm 7.2's clang
+// bit-casts the vector's first element whatever the index (it takes the
+// element's address as the vector's).  The first version of this hand-over
+// bit-cast element 2 of the last float4 to read the status and got the
+// speed's low word: every row's landed / crashed columns were wrong
+// (tests/test_gpu_configs.py config 2 caught it; tests/test_source_lint.py
+// now rejects the pattern).  Elements go through __uint_as_float / plain
+// integer conversions.
+__device__ __forceinline__ u32x4 words2(double a, double b) {
+    const uint64_t x = __builtin_bit_cast(uint64_t, a), y = __builtin_bit_cast(uint64_t, b);
+    return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+}
+__device__ __forceinline__ double word_pair(uint32_t lo, uint32_t hi) {
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ D2 unpack2(u32x4 w) { return D2{word_pair(w[0], w[1]), word_pair(w[2], w[3])}; }
+
 template <typename T>
 __device__ __forceinline__ void stage_put(f32x4* slot, uint32_t lane, const Lane& s, T reward) {
-    slot[0 * kWave + lane] = pack2(s.x, s.y);
-    slot[1 * kWave + lane] = pack2(s.vx, s.vy);
-    slot[2 * kWave + lane] = pack2(s.angle, s.omega);
-    slot[3 * kWave + lane] = pack2(s.fuel, s.px);
-    slot[4 * kWave + lane] = pack2(s.py, s.dist);
-    f32x4 q5 = pack2(s.speed, 0.0);
-    q5[2] = __builtin_bit_cast(float, s.status);
-    if constexpr (std::is_same<T, float>::value) q5[3] = reward;
-    slot[5 * kWave + lane] = q5;
-    if constexpr (std::is_same<T, double>::value) slot[6 * kWave + lane] = pack2(reward, 0.0);
+    const auto put = [&](int q, u32x4 w) { slot[q * kWave + lane] = __builtin_bit_cast(f32x4, w); };
+    put(0, words2(s.x, s.y));
+    put(1, words2(s.vx, s.vy));
+    put(2, words2(s.angle, s.omega));
+    put(3, words2(s.fuel, s.px));
+    put(4, words2(s.py, s.dist));
+    const uint64_t sp = __builtin_bit_cast(uint64_t, s.speed);
+    if constexpr (std::is_same<T, float>::value) {
+        put(5, u32x4{(uint32_t)sp, (uint32_t)(sp >> 32), s.status, __builtin_bit_cast(uint32_t, reward)});
+    } else {
+        put(5, u32x4{(uint32_t)sp, (uint32_t)(sp >> 32), s.status, 0u});
+        put(6, words2(reward, 0.0));
+    }
 }
 
 template <typename T>
 __device__ __forceinline__ void stage_get(const f32x4* slot, uint32_t lane, Lane& s, T& reward) {
-    f32x4 q[kStageQ<T>];
+    u32x4 q[kStageQ<T>];
 #pragma unroll
-    for (int j = 0; j < kStageQ<T>; ++j) q[j] = slot[j * kWave + lane];
+    for (int j = 0; j < kStageQ<T>; ++j) q[j] = __builtin_bit_cast(u32x4, slot[j * kWave + lane]);
     D2 d = unpack2(q[0]);
     s.x = d.a, s.y = d.b;
     d = unpack2(q[1]);
@@ -671,10 +689,10 @@ __device__ __forceinline__ void stage_get(const f32x4* slot, uint32_t lane, Lane
     s.fuel = d.a, s.px = d.b;
     d = unpack2(q[4]);
     s.py = d.a, s.dist = d.b;
-    s.speed = unpack2(q[5]).a;
-    s.status = __builtin_bit_cast(uint32_t, q[5][2]);
-    if constexpr (std::is_same<T, float>::value) reward = q[5][3];
-    else reward = unpack2(q[6]).a;
+    s.speed = word_pair(q[5][0], q[5][1]);
+    s.status = q[5][2];
+    if constexpr (std::is_same<T, float>::value) reward = __uint_as_float(q[5][3]);
+    else reward = word_pair(q[6][0], q[6][1]);
 }
 
 #ifndef DD_ROLL_MIN_WAVES
