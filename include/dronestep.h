@@ -306,8 +306,7 @@ typedef struct DDMlpIO {
  * rows 35.8 -> 15-18 us on MI355X): each
  * operand split into two f16 halves, a = hi + lo * 2^-11, three f16 MFMAs
  * per product with f32 accumulation (~22 bits per product, about the f32
- * path's end-to-end error); hidden-layer |weights| < 16 (their f16 hi halves are
- * packed times 2^11), |obs| and activations < 65504.
+ * path's end-to-end error); |weights|, |obs| and activations < 65504.
  * LayerNorm, the last layer and sampling are f32 either way. */
 enum { DD_MLP_F32 = 0, DD_MLP_F16X3 = 1 };
 

@@ -87,23 +87,6 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr float kLoScale = 2048.0f;  // 2^11: lo' lives at hi's magnitude (no f16 subnormals)
 constexpr float kLoUnscale = 1.0f / 2048.0f;
-// kHiScaled: the packed weights' hi halves, the Linear biases and the
-// LayerNorm eps are stored scaled (hi * 2^11, bias * 2^11, eps * 2^22), so
-// a layer's accumulator holds 2^11 times its output with no rescaling pass:
-// it starts at the scaled bias, takes the cross terms (hi.lo' + lo'.hi, at
-// 2^11 already) and the scaled hi.hi products.  Every scaling is by a power
-// of two (exact); LayerNorm((2^11 x); 2^22 eps) = LayerNorm(x; eps), so only
-// the accumulation order differs (the bias is now the first term, not the
-// last but hi.hi).  Saves the 16 fmaf per 32-row tile of the rescale (160
-// VALU per tile).  Weights must be below 32 in magnitude (2^11 hi within the
-// f16 range); MlpNet checks.  DD_MLP_LO_UNSCALE: the rescaling pass (A/B).
-#ifdef DD_MLP_LO_UNSCALE
-constexpr bool kHiScaled = false;
-#else
-constexpr bool kHiScaled = true;
-#endif
-constexpr float kBiasScale = kHiScaled ? 2048.0f : 1.0f;
-constexpr float kEpsScale = kHiScaled ? 4194304.0f : 1.0f;  // 2^22
 
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
@@ -185,7 +168,7 @@ __device__ __forceinline__ void layer16(const u32x4* __restrict__ a16, int lane,
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = kHiScaled ? bias_h[hid(t, r, 0)] : 0.0f;
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
@@ -198,12 +181,10 @@ __device__ __forceinline__ void layer16(const u32x4* __restrict__ a16, int lane,
         }
         __builtin_amdgcn_sched_barrier(0);  // keep each k-step's LDS reads next to its MFMAs
     }
-    if constexpr (!kHiScaled) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
-    }
+        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
@@ -327,11 +308,11 @@ struct NoMid {
 template <int NTO>
 __device__ __forceinline__ void norm_split_cross(const f32x16 (&acc)[4], const float* vec, float eps, int h,
                                                  const u32x4* __restrict__ a16n, int lane, f16x8 (&bh)[8],
-                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO], const float* bias_n) {
+                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO]) {
 #pragma unroll
     for (int to = 0; to < NTO; ++to)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) out[to][r] = kHiScaled ? bias_n[hid(to, r, 0)] : 0.0f;
+        for (int r = 0; r < 16; ++r) out[to][r] = 0.0f;
     auto emit = [&](int t, const float (&v)[16]) {
         split8(&v[0], bh[2 * t], bl[2 * t]);
         split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
@@ -351,17 +332,15 @@ __device__ __forceinline__ void norm_split_cross(const f32x16 (&acc)[4], const f
     norm_relu_emit<4, decltype(emit), false>(acc, vec, eps, h, emit);
 }
 
-// The rest of layer16 after its cross terms: (unless kHiScaled) scale them
-// by 2^-11 and add the bias; accumulate the hi.hi products.
+// The rest of layer16 after its cross terms: scale them by 2^-11, add the
+// bias, accumulate the hi.hi products.
 template <int NT, int KS>
 __device__ __forceinline__ void layer16_hihi(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
                                              f32x16 (&acc)[NT], const float* bias_h) {
-    if constexpr (!kHiScaled) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
-    }
+        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
@@ -422,7 +401,7 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
         constexpr bool kPipelined = kPipe;
 #endif
         if constexpr (kPipelined) {
-            norm_split_cross<2>(acc4, lds + kV2, eps, h, a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+            norm_split_cross<2>(acc4, lds + kV2, eps, h, a16 + kA3 / 4, lane, bh, bl, acc2);
             layer16_hihi<2, 8>(a16 + kA3 / 4, lane, bh, acc2, lds + kV3 + 4 * h);
         } else {  // layer 2's LayerNorm + split, then all of layer 3
             norm_relu_split<4>(acc4, lds + kV2, eps, h, bh, bl);

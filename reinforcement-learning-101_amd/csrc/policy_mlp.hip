@@ -90,10 +90,6 @@ __device__ __forceinline__ float pack_a16(const DDMlpParams& p, int i) {
     }
     uint32_t hi, lo;
     split_pair(v[0], v[1], hi, lo);
-    if (kHiScaled) {  // hi * 2^11: exact below 32 in magnitude (MlpNet checks the weights)
-        const f16x2 h = __builtin_bit_cast(f16x2, hi);
-        hi = __builtin_bit_cast(uint32_t, f16x2{(_Float16)((float)h.x * kLoScale), (_Float16)((float)h.y * kLoScale)});
-    }
     return __uint_as_float(part == 0 ? hi : lo);
 }
 
@@ -102,9 +98,7 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= kPacked) return;
     float v = 0.0f;
-    const bool f16 = compute == DD_MLP_F16X3;
-    const float bs = f16 ? kBiasScale : 1.0f;
-    if (i < kV1 && f16) {
+    if (i < kV1 && compute == DD_MLP_F16X3) {
         v = pack_a16(p, i);
     } else if (i < kV1) {  // A operands: lane l of k-step q of out tile t holds W[32t + (l&31)][k(q, l>>5)]
         const int base = i < kA2 ? kA1 : i < kA3 ? kA2 : kA3;
@@ -117,24 +111,24 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
         // (t', r) = q takes hidden row hid(t', r, h)
         const int col = base == kA1 ? 2 * q + h : hid(q >> 4, q & 15, h);
         v = weight_at(p, base, row, col);
-    } else if (i < kV2) {  // (f16x3: the hidden Linear biases and the eps stored scaled, kHiScaled)
+    } else if (i < kV2) {
         const int o = i - kV1;
         const float* src[3] = {p.b0, p.ln1_w, p.ln1_b};
-        v = o < 128 ? bias_at(p.b0, 128, o) * bs : src[o / 128][o % 128];
+        v = o < 128 ? bias_at(p.b0, 128, o) : src[o / 128][o % 128];
     } else if (i < kV3) {
         const int o = i - kV2;
         const float* src[3] = {p.b3, p.ln4_w, p.ln4_b};
-        v = o < 128 ? bias_at(p.b3, 128, o) * bs : src[o / 128][o % 128];
+        v = o < 128 ? bias_at(p.b3, 128, o) : src[o / 128][o % 128];
     } else if (i < kW4) {
         const int o = i - kV3;
         const float* src[3] = {p.b6, p.ln7_w, p.ln7_b};
-        v = o < 64 ? bias_at(p.b6, 64, o) * bs : src[o / 64][o % 64];
+        v = o < 64 ? bias_at(p.b6, 64, o) : src[o / 64][o % 64];
     } else if (i < kB4) {
         const int o = i - kW4;
         v = (o / 64) < p.out_dim ? p.w9[o] : 0.0f;
     } else if (i < kTag) {
         const int o = i - kB4;
-        v = o < p.out_dim ? p.b9[o] : (o == 3 ? p.ln_eps * (f16 ? kEpsScale : 1.0f) : 0.0f);
+        v = o < p.out_dim ? p.b9[o] : (o == 3 ? p.ln_eps : 0.0f);
     } else {
         v = i == kTag ? __uint_as_float(pack_tag(compute, p.out_dim)) : 0.0f;
     }

@@ -77,15 +77,14 @@ class MlpNet:
                      for k in STATE_DICT_KEYS}
         if compute == "f16x3":
             # the hidden Linears' weights go into f16 halves after centring over
-            # their outputs (|w - mean| <= 2 max|w|), the hi half stored times
-            # 2^11 (mlp_core.h kHiScaled): past the f16 range it is inf and every
-            # probability NaN, so refuse such weights here (the notebooks' largest
-            # is 3.8; observations and activations must stay below 65504)
+            # their outputs (|w - mean| <= 2 max|w|): beyond the f16 range the hi
+            # half is inf and every probability NaN, so refuse such weights here
+            # (observations and activations must stay below 65504 as well)
             for k in ("0.weight", "3.weight", "6.weight"):
                 w = self._src[k]
-                if not bool(torch.isfinite(w).all()) or float(w.abs().max()) >= 16.0:
-                    raise ValueError(f"{k}: compute='f16x3' needs finite weights below 16 in magnitude "
-                                     "(2^11 times the centred weight within the f16 range); use compute='f32'")
+                if not bool(torch.isfinite(w).all()) or float(w.abs().max()) >= 65504.0 / 2:
+                    raise ValueError(f"{k}: compute='f16x3' needs finite weights below 32752 in magnitude "
+                                     "(the f16 range after centring); use compute='f32'")
         p = abi.DDMlpParams(*[self._src[k].data_ptr() for k in STATE_DICT_KEYS], self.out_dim, self.ln_eps)
         self.packed = torch.empty(int(self._lib.dd_mlp_packed_floats()), dtype=torch.float32, device=self.device)
         abi.check(self._lib.dd_mlp_pack(ctypes.byref(p), self._mode, self.packed.data_ptr(), self._stream()),

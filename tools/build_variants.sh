@@ -7,8 +7,8 @@ OUT=delivery_drone_amd/_native/lab
 mkdir -p $OUT
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I../include -Ibuild"
 build() { /opt/rocm/bin/hipcc $FLAGS "${@:2}" -o $OUT/lib_$1.so csrc/drone_step.hip csrc/policy_mlp.hip csrc/policy_rollout.hip csrc/render.hip & }
-# "prev": the committed source at $PREV_REV (default HEAD; "none" skips it), for before/after runs
-if [ "${PREV_REV:-HEAD}" != none ] && git -C .. rev-parse -q --verify "${PREV_REV:-HEAD}" > /dev/null 2>&1; then
+# "prev": the committed source at $PREV_REV (default HEAD), for before/after runs
+if [ -n "${PREV_REV:-HEAD}" ] && git -C .. rev-parse -q --verify "${PREV_REV:-HEAD}" > /dev/null 2>&1; then
   mkdir -p /tmp/dd_prev
   git -C .. show "${PREV_REV:-HEAD}:reinforcement-learning-101_amd/csrc/drone_step.hip" > /tmp/dd_prev/drone_step.hip
   PREV_SRCS=/tmp/dd_prev/drone_step.hip
@@ -27,7 +27,6 @@ for v in ${VARIANTS:-base}; do
     s0lds) build s0lds -DDD_EXP_S0_LDS ;;
     flats0) build flats0 -DDD_EXP_FLAT_NEAR -DDD_EXP_S0_LDS ;;
     sel) build sel -DDD_EXP_SEL ;;
-    lounscale) build lounscale -DDD_MLP_LO_UNSCALE ;;
     ocml) build ocml -DDD_TRIG_OCML ;;
     plainobs) build plainobs -DDD_ST_OBS=0 ;;
     nofma) build nofma -DDD_TRIG_NO_FMA ;;
