@@ -836,6 +836,13 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
                  "v"(s.px), "v"(s.py), "v"(s.total), "v"(s.status), "v"(s.steps), "v"(s.episode), "v"(act0),
                  "v"(act1));
     if constexpr (kParked) quantize_park<T, false>(s, rec);  // frame 0's starting state (already quantized)
+    // auto_reset: the next episode's Philox block per lane (frame.h).  Not with
+    // the in-kernel Philox actions, whose own blocks it competes with for
+    // registers: there it cost 2-3 % (65,536 and 262,144 x 256), where with
+    // action buffers it took 65,536 x 256 from 0.330 to 0.303 ms
+    // (profiles/r04/lab/roll_spawn_ahead.jsonl)
+    constexpr bool kAhead = AFMT != DD_ACT_PHILOX;
+    SpawnAhead ahead;
     // One frame; kObs and kAuto (auto_reset) are compile-time so the loop
     // body carries no uniform branch on them.
     auto run_frame = [&](const int f, uint32_t& slot, auto obs_c, auto auto_c) __attribute__((always_inline)) {
@@ -870,7 +877,8 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             reward = fast();
             if (__ballot(was_done)) {
                 if (was_done) {
-                    spawn(sw, k.c.max_fuel, env, s);
+                    if constexpr (kAhead) ahead.respawn(sw, k.c.max_fuel, env, s);
+                    else spawn(sw, k.c.max_fuel, env, s);
                     reward = 0.0;
                 }
             }
@@ -945,8 +953,10 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             erew_p += p.reward_stride;
             edone_p += p.n_total;
         }
+        if constexpr (kAuto && kAhead) ahead.refill(sw, env, s.episode, f);
     };
     auto run = [&](auto obs_c, auto auto_c) __attribute__((always_inline)) {
+        if constexpr (decltype(auto_c)::value && kAhead) ahead.init(sw, env, s.episode);
         // an odd count leaves the loop between the pair's frames (`break`, not
         // a skipped second frame): the loop latch is then reached from one
         // path only, and the vmcnt the compiler derives there for the

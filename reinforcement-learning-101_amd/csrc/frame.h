@@ -240,18 +240,22 @@ __device__ __forceinline__ double measure(Lane& s) {
 // a rollout's frame loop issues no scalar load that a join's lgkmcnt wait
 // would couple to its LDS reads); s.episode becomes the value after
 // `episode += 1`.
-__device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_t env, Lane& s) {
-    s.episode += 1;
-    uint32_t r[4];
+// The Philox block of (seed; env, episode) that a re-spawn draws from.
+__device__ __forceinline__ void spawn_words(const DDConfig& c, int64_t env, int32_t episode, uint32_t (&r)[4]) {
 #ifdef DD_EXP_FAKE_SPAWN  // timing-only sensitivity: what the re-spawn's Philox block costs
-    r[0] = (uint32_t)env * 0x9E3779B9u ^ (uint32_t)s.episode;
+    r[0] = (uint32_t)env * 0x9E3779B9u ^ (uint32_t)episode;
     r[1] = r[0] * 0x85EBCA6Bu;
     r[2] = r[1] * 0xC2B2AE35u;
     r[3] = r[2] * 0x27D4EB2Fu;
 #else
-    philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)s.episode, 0u,
-                  (uint32_t)c.seed, (uint32_t)(c.seed >> 32), r);
+    philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)episode, 0u, (uint32_t)c.seed,
+                  (uint32_t)(c.seed >> 32), r);
 #endif
+}
+
+// The re-spawn of a lane whose episode counter is already the new episode's,
+// from that episode's Philox block r (spawn_words).
+__device__ __forceinline__ void spawn_from(const DDConfig& c, double max_fuel, const uint32_t (&r)[4], Lane& s) {
     if (c.randomize_drone) {
         s.x = draw_range(r[0], c.drone_x_min, (uint32_t)(c.drone_x_max - c.drone_x_min + 1));
         s.y = draw_range(r[1], c.drone_y_min, (uint32_t)(c.drone_y_max - c.drone_y_min + 1));
@@ -282,6 +286,49 @@ __device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_
     s.dist = trig::sqrt_unscaled(dx * dx + dy * dy);
 #endif
 }
+
+__device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_t env, Lane& s) {
+    s.episode += 1;
+    uint32_t r[4];
+    spawn_words(c, env, s.episode, r);
+    spawn_from(c, max_fuel, r, s);
+}
+
+// A rollout loop's re-spawns with the Philox block drawn ahead.  Under
+// auto-reset most waves have a lane to re-spawn in most frames (a wave of 64
+// drones, episodes of tens to hundreds of frames), and the wave runs the
+// re-spawn's Philox block (~60 VALU) for it.  Here each lane keeps the block
+// of its NEXT episode (r, drawn for episode `ep`); a re-spawn takes it, and
+// every kRefill-th frame the lanes whose block is spent draw the next one
+// together: one Philox per wave per kRefill frames instead of one per frame.
+// A lane ending two episodes within kRefill frames draws in-frame (the old
+// path).  Same blocks, same spawns: the results are bit for bit spawn()'s.
+struct SpawnAhead {
+    uint32_t r[4];
+    int32_t ep;  // the episode r was drawn for
+    static constexpr int kRefill = 8;
+
+    __device__ __forceinline__ void init(const DDConfig& c, int64_t env, int32_t episode) {
+        ep = episode + 1;
+        spawn_words(c, env, ep, r);
+    }
+    // frame f's end (wave-uniform f): refill the spent blocks
+    __device__ __forceinline__ void refill(const DDConfig& c, int64_t env, int32_t episode, int f) {
+        if ((f & (kRefill - 1)) == kRefill - 1) {
+            const bool spent = ep != episode + 1;
+            if (__ballot(spent)) {
+                if (spent) init(c, env, episode);
+            }
+        }
+    }
+    // the auto-reset re-spawn of a done lane (called by that lane only)
+    __device__ __forceinline__ void respawn(const DDConfig& c, double max_fuel, int64_t env, Lane& s) {
+        s.episode += 1;
+        uint32_t w[4] = {r[0], r[1], r[2], r[3]};
+        if (ep != s.episode) spawn_words(c, env, s.episode, w);  // spent: draw now
+        spawn_from(c, max_fuel, w, s);
+    }
+};
 
 // physics.normalize_angle after one frame's turn.  |omega| stays near
 // 0.3 / (1 - 0.95) = 6 degrees per frame, so the angle leaves (-540, 540]

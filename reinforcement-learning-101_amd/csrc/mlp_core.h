@@ -369,6 +369,24 @@ __device__ __forceinline__ float bernoulli_logp(float p, bool on) {
 }
 
 
+// Linear(64, K) of one tile from its LayerNorm'd layer-3 rows: 32 rows per
+// lane half, then the other half's.
+template <int K>
+__device__ __forceinline__ void head_of(const float* lds, int h, const float (&y3)[2][16], float (&z)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const float* w = lds + kW4 + k * 64 + 4 * h;
+        f32x2 s2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2)
+                s2 = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(w + hid(t, r, 0)),
+                                               f32x2{y3[t][r], y3[t][r + 1]}, s2);
+        z[k] = add_other_half(s2.x + s2.y) + lds[kB4 + k];
+    }
+}
+
 // The network up to the last layer's outputs z (before the actor's Sigmoid)
 // for the 32 drones of one wave tile: lane (c, h) holds column c's inputs
 // x[q] = obs[c][2q + h] (DD_MLP_F32, k-steps of 2) or obs[c][8h + q]
@@ -421,18 +439,134 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
         norm_relu<2>(acc2, lds + kV3, eps, h, y3);
     }
     __builtin_amdgcn_sched_barrier(0);
+    head_of<K>(lds, h, y3, z);
+}
+
+// ---- Two tiles per wave (f16x3): one tile's MFMAs against the other's VALU --
+// A gfx950 SIMD overlaps a wave's VALU with that wave's own earlier,
+// independent MFMAs, never with another wave's ("What the
+// actor's time is made of").  With one tile per wave nearly every VALU
+// instruction waits for the MFMAs just before it, so a tile costs its VALU
+// plus its MFMA time.  mlp_pair runs two tiles (A, B) in one wave, half a
+// layer apart:
+//   L1(A) | L1(B) + LN1(A) | L2(A) + LN1(B) | L2(B) + LN2(A) | L3(A) + LN2(B) |
+//   L3(B) + LN3(A) + head(A) | LN3(B) + head(B)
+// and inside each phase the one tile's MFMAs are issued one by one between
+// slices of the other tile's LayerNorm / split (sched_group_barrier), so the
+// VALU runs in the MFMA pipe's shadow.  Every accumulator sees the same MFMAs
+// in the same order as layer16's, and the LayerNorm / split / head are the same
+// code (mlp_body's), so both tiles come out bit for bit as mlp_body's.
+
+// layer16 without its scheduling fences (the phase's interleave orders it)
+template <int NT, int KS>
+__device__ __forceinline__ void layer16_free(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
+                                             const f16x8 (&bl)[KS], f32x16 (&acc)[NT], const float* bias_h) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {  // Linear(64, K): 32 rows per lane half, then the other half's
-        const float* w = lds + kW4 + k * 64 + 4 * h;
-        f32x2 s2 = {0.0f, 0.0f};
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 #pragma unroll
-            for (int r = 0; r < 16; r += 2)
-                s2 = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(w + hid(t, r, 0)),
-                                               f32x2{y3[t][r], y3[t][r + 1]}, s2);
-        z[k] = add_other_half(s2.x + s2.y) + lds[kB4 + k];
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const u32x4* blk = a16 + (t * KS + s) * 128;
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, blk[lane]), bl[s], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, blk[64 + lane]), bh[s], acc[t], 0,
+                                                            0, 0);
+        }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a16[(t * KS + s) * 128 + lane]),
+                                                            bh[s], acc[t], 0, 0, 0);
+}
+
+#ifndef DD_MLP_PAIR_VALU
+#define DD_MLP_PAIR_VALU 4  // VALU instructions placed after each MFMA of a phase (lab knob)
+#endif
+
+// The interleave of one phase: NM times (one MFMA, then up to NV VALU).
+template <int NM, int NV>
+__device__ __forceinline__ void interleave_mfma_valu() {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);  // VALU
     }
+}
+
+template <int NT>
+__device__ __forceinline__ void norm_split_free(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
+                                                f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
+    auto emit = [&](int t, const float (&v)[16]) {
+        split8(&v[0], bh[2 * t], bl[2 * t]);
+        split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
+    };
+    norm_relu_emit<NT, decltype(emit), false>(acc, vec, eps, h, emit);
+}
+
+template <int NT>
+__device__ __forceinline__ void norm_free(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
+                                          float (&y)[NT][16]) {
+    auto emit = [&](int t, const float (&v)[16]) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[t][r] = v[r];
+    };
+    norm_relu_emit<NT, decltype(emit), false>(acc, vec, eps, h, emit);
+}
+
+// Two tiles' networks (f16x3) up to the last layer's outputs: lane (c, h)
+// holds column c's inputs xa / xb as mlp_body's kSplit path; za / zb as its z.
+template <int K, typename Mid = NoMid>
+__device__ __forceinline__ void mlp_pair(const float* lds, int lane, const float (&xa)[8], const float (&xb)[8],
+                                         float (&za)[K], float (&zb)[K], Mid mid = {}) {
+    constexpr int NV = DD_MLP_PAIR_VALU;
+    const u32x4* a16 = reinterpret_cast<const u32x4*>(lds);
+    const int h = lane >> 5;
+    const float eps = lds[kB4 + 3];
+    f32x16 accA[4], accB[4], acc2A[2], acc2B[2];
+    f16x8 bhA[8], blA[8], bhB[8], blB[8];
+    float y3A[2][16], y3B[2][16];
+    {
+        f16x8 ih[1], il[1];
+        split8(xa, ih[0], il[0]);
+        layer16_free<4, 1>(a16 + kA1 / 4, lane, ih, il, accA, lds + kV1 + 4 * h);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        f16x8 ih[1], il[1];
+        split8(xb, ih[0], il[0]);
+        layer16_free<4, 1>(a16 + kA1 / 4, lane, ih, il, accB, lds + kV1 + 4 * h);
+        norm_split_free<4>(accA, lds + kV1, eps, h, bhA, blA);
+        interleave_mfma_valu<12, NV>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mid();
+    __builtin_amdgcn_sched_barrier(0);
+    layer16_free<4, 8>(a16 + kA2 / 4, lane, bhA, blA, accA, lds + kV2 + 4 * h);
+    norm_split_free<4>(accB, lds + kV1, eps, h, bhB, blB);
+    interleave_mfma_valu<96, NV>();
+    __builtin_amdgcn_sched_barrier(0);
+    layer16_free<4, 8>(a16 + kA2 / 4, lane, bhB, blB, accB, lds + kV2 + 4 * h);
+    norm_split_free<4>(accA, lds + kV2, eps, h, bhA, blA);
+    interleave_mfma_valu<96, NV>();
+    __builtin_amdgcn_sched_barrier(0);
+    layer16_free<2, 8>(a16 + kA3 / 4, lane, bhA, blA, acc2A, lds + kV3 + 4 * h);
+    norm_split_free<4>(accB, lds + kV2, eps, h, bhB, blB);
+    interleave_mfma_valu<48, NV>();
+    __builtin_amdgcn_sched_barrier(0);
+    layer16_free<2, 8>(a16 + kA3 / 4, lane, bhB, blB, acc2B, lds + kV3 + 4 * h);
+    norm_free<2>(acc2A, lds + kV3, eps, h, y3A);
+    head_of<K>(lds, h, y3A, za);
+    interleave_mfma_valu<48, NV>();
+    __builtin_amdgcn_sched_barrier(0);
+    norm_free<2>(acc2B, lds + kV3, eps, h, y3B);
+    head_of<K>(lds, h, y3B, zb);
 }
 
 // The actor's head: Sigmoid probabilities of the last layer's outputs.

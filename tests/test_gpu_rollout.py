@@ -248,6 +248,26 @@ def test_rollout_switches(cfg, n, precision, gpu_device):
     assert_same_state(roll, loop)
 
 
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("n", [777, 65_532])
+def test_rollout_short_episodes_equal_step_loop(precision, n, gpu_device):
+    """Episodes of a few frames (max_fuel 1.5: out of fuel after one or two
+    thrusting frames), so lanes end several episodes between two refills of
+    the rollout's drawn-ahead re-spawn blocks (frame.h SpawnAhead, every 8th
+    frame): both the drawn-ahead and the in-frame draw, bit for bit the step
+    loop's; 65,532 lanes take the split kernel when the config allows it."""
+    k = 37
+    roll, loop = twins(n, gpu_device, precision, randomize_drone=True, randomize_platform=True, auto_reset=True,
+                       seed=23, max_fuel=1.5)
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
+    obs, reward, done = roll.rollout(acts)
+    for t in range(k):
+        o, r, d, _ = loop.step(acts[t])
+        assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
+    assert_same_state(roll, loop)
+    assert int(roll.episode.max()) >= 8  # several episodes per 8 frames on some lanes
+
+
 def test_step_out_buffers_equal_rollout(gpu_device):
     """BASELINE config 5(a): one dd_step per frame writing straight into the
     rollout buffers (step(out=...)) equals one dd_rollout launch."""

@@ -17,6 +17,8 @@
 #   lab        tools/kernel_lab.py (VARIANTS, ENVS, LABARGS)
 #   roll       tools/rollout_lab.py (VARIANTS, ENVS, ROLLARGS e.g. --philox), appended to <tag>/roll.jsonl
 #   sqroll     SQ counters of dd_rollout per lab variant (tools/pmc_rollout_ab.sh; ROLLARGS, ROLLSUFFIX)
+#   roll5      config 5 only: rocprof kernel trace of 20 dd_rollout launches (65,536 x 256) and the
+#              rollout kernel's FETCH_SIZE / WRITE_SIZE passes (tools/prof_driver.py --what rollout)
 #   mr         tools/multirank_check.py on 2 gloo ranks sharing GPU 0 (torchrun), output in <tag>/mr/
 #   py:<file>  python <file> (LABARGS passed through), output in <tag>/<file stem>.log
 set -o pipefail
@@ -60,6 +62,14 @@ run_step() {
         done ;;
     sq)
         bash tools/pmc_sq.sh $OUT ;;
+    roll5)
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_c5 -o roll -f csv -- python3 tools/prof_driver.py \
+            --what rollout --envs 65536 --frames 256 --reps 20 > /dev/null 2> $OUT/roll5.err || return 1
+        for C in FETCH_SIZE WRITE_SIZE; do
+            timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex rollout_kernel -d $OUT/pmc_roll_$C -o pmc -f csv \
+                -- python3 tools/prof_driver.py --what rollout --envs 65536 --frames 256 --reps 5 > /dev/null \
+                2>> $OUT/roll5.err || return 1
+        done ;;
     lab)
         timeout -k 10 600 python tools/kernel_lab.py --variants ${VARIANTS:-base} --envs ${ENVS:-262144,1048576,16777216} \
             ${LABARGS} > $OUT/lab.jsonl 2> $OUT/lab.err; local rc=$?; cat $OUT/lab.jsonl; tail -5 $OUT/lab.err; return $rc ;;
