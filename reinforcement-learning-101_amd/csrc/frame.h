@@ -299,14 +299,17 @@ __device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_
 // drones, episodes of tens to hundreds of frames), and the wave runs the
 // re-spawn's Philox block (~60 VALU) for it.  Here each lane keeps the block
 // of its NEXT episode (r, drawn for episode `ep`); a re-spawn takes it, and
-// every kRefill-th frame the lanes whose block is spent draw the next one
+// every kRefill-th frame (32) the lanes whose block is spent draw the next one
 // together: one Philox per wave per kRefill frames instead of one per frame.
 // A lane ending two episodes within kRefill frames draws in-frame (the old
 // path).  Same blocks, same spawns: the results are bit for bit spawn()'s.
 struct SpawnAhead {
     uint32_t r[4];
     int32_t ep;  // the episode r was drawn for
-    static constexpr int kRefill = 8;
+#ifndef DD_SPAWN_REFILL
+#define DD_SPAWN_REFILL 32  // frames between refills (a power of two; lab knob)
+#endif
+    static constexpr int kRefill = DD_SPAWN_REFILL;
 
     __device__ __forceinline__ void init(const DDConfig& c, int64_t env, int32_t episode) {
         ep = episode + 1;

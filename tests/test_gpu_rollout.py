@@ -253,7 +253,7 @@ def test_rollout_switches(cfg, n, precision, gpu_device):
 def test_rollout_short_episodes_equal_step_loop(precision, n, gpu_device):
     """Episodes of a few frames (max_fuel 1.5: out of fuel after one or two
     thrusting frames), so lanes end several episodes between two refills of
-    the rollout's drawn-ahead re-spawn blocks (frame.h SpawnAhead, every 8th
+    the rollout's drawn-ahead re-spawn blocks (frame.h SpawnAhead, every 32nd
     frame): both the drawn-ahead and the in-frame draw, bit for bit the step
     loop's; 65,532 lanes take the split kernel when the config allows it."""
     k = 37
@@ -265,7 +265,7 @@ def test_rollout_short_episodes_equal_step_loop(precision, n, gpu_device):
         o, r, d, _ = loop.step(acts[t])
         assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
     assert_same_state(roll, loop)
-    assert int(roll.episode.max()) >= 8  # several episodes per 8 frames on some lanes
+    assert int(roll.episode.max()) >= 8  # several episodes between two refills on some lanes
 
 
 def test_step_out_buffers_equal_rollout(gpu_device):

@@ -75,6 +75,7 @@ for v in ${VARIANTS:-base}; do
     iterilp) build iterilp -mllvm -amdgpu-sched-strategy=iterative-ilp ;;
     itermin) build itermin -mllvm -amdgpu-sched-strategy=iterative-minreg ;;
     mpad*) build $v -DDD_MLP_PAD=${v#mpad} ;;
+    ref*) build $v -DDD_SPAWN_REFILL=${v#ref} ;;
     log1p) build log1p -DDD_MLP_LOG1P ;;
     serial) build serial -DDD_MLP_SERIAL ;;
     splitcvt) build splitcvt -DDD_MLP_SPLIT_CVT ;;
