@@ -136,11 +136,11 @@ __device__ __forceinline__ void store_dynamics(const Soa<T>& a, uint32_t i, cons
     put_state(a.fuel, i, (T)s.fuel);
 }
 
-template <typename T>
+template <typename T, bool kTotal = true>
 __device__ __forceinline__ void store_spawn(const Soa<T>& a, uint32_t i, const Lane& s) {
     store_dynamics(a, i, s);
     at(a.px, i) = (T)s.px; at(a.py, i) = (T)s.py;
-    at(a.total, i) = (T)s.total;
+    if constexpr (kTotal) at(a.total, i) = (T)s.total;
     at(a.status, i) = (uint8_t)s.status;
     at(a.steps, i) = s.steps;
     at(a.episode, i) = s.episode;
@@ -622,8 +622,7 @@ __device__ __forceinline__ uint32_t buffer_action(__amdgpu_buffer_rsrc_t r, uint
 // Every wait is bounded (kSpinCap polls of ~64 clocks, ~30 ms): a broken
 // hand-over ends the kernel with wrong rows, never a wave that spins forever.
 constexpr int kSpinCap = 1 << 20;
-template <typename T>
-constexpr int kStageQ = std::is_same<T, double>::value ? 7 : 6;
+constexpr int kStageQ = 5;
 
 struct D2 {
     double a, b;
@@ -657,28 +656,23 @@ __device__ __forceinline__ double word_pair(uint32_t lo, uint32_t hi) {
 }
 __device__ __forceinline__ D2 unpack2(u32x4 w) { return D2{word_pair(w[0], w[1]), word_pair(w[2], w[3])}; }
 
-template <typename T>
-__device__ __forceinline__ void stage_put(f32x4* slot, uint32_t lane, const Lane& s, T reward) {
+// The frame's state as frame() leaves it under kDefer (unrounded), and the
+// status word with kWasDone when the lane started the frame done: 5 float4.
+constexpr uint32_t kWasDone = 1u << 8;
+__device__ __forceinline__ void stage_put(f32x4* slot, uint32_t lane, const Lane& s, uint32_t status) {
     const auto put = [&](int q, u32x4 w) { slot[q * kWave + lane] = __builtin_bit_cast(f32x4, w); };
     put(0, words2(s.x, s.y));
     put(1, words2(s.vx, s.vy));
     put(2, words2(s.angle, s.omega));
     put(3, words2(s.fuel, s.px));
-    put(4, words2(s.py, s.dist));
-    const uint64_t sp = __builtin_bit_cast(uint64_t, s.speed);
-    if constexpr (std::is_same<T, float>::value) {
-        put(5, u32x4{(uint32_t)sp, (uint32_t)(sp >> 32), s.status, __builtin_bit_cast(uint32_t, reward)});
-    } else {
-        put(5, u32x4{(uint32_t)sp, (uint32_t)(sp >> 32), s.status, 0u});
-        put(6, words2(reward, 0.0));
-    }
+    const uint64_t py = __builtin_bit_cast(uint64_t, s.py);
+    put(4, u32x4{(uint32_t)py, (uint32_t)(py >> 32), status, 0u});
 }
 
-template <typename T>
-__device__ __forceinline__ void stage_get(const f32x4* slot, uint32_t lane, Lane& s, T& reward) {
-    u32x4 q[kStageQ<T>];
+__device__ __forceinline__ void stage_get(const f32x4* slot, uint32_t lane, Lane& s, uint32_t& status) {
+    u32x4 q[kStageQ];
 #pragma unroll
-    for (int j = 0; j < kStageQ<T>; ++j) q[j] = __builtin_bit_cast(u32x4, slot[j * kWave + lane]);
+    for (int j = 0; j < kStageQ; ++j) q[j] = __builtin_bit_cast(u32x4, slot[j * kWave + lane]);
     D2 d = unpack2(q[0]);
     s.x = d.a, s.y = d.b;
     d = unpack2(q[1]);
@@ -687,12 +681,8 @@ __device__ __forceinline__ void stage_get(const f32x4* slot, uint32_t lane, Lane
     s.angle = d.a, s.omega = d.b;
     d = unpack2(q[3]);
     s.fuel = d.a, s.px = d.b;
-    d = unpack2(q[4]);
-    s.py = d.a, s.dist = d.b;
-    s.speed = word_pair(q[5][0], q[5][1]);
-    s.status = q[5][2];
-    if constexpr (std::is_same<T, float>::value) reward = __uint_as_float(q[5][3]);
-    else reward = word_pair(q[6][0], q[6][1]);
+    s.py = word_pair(q[4][0], q[4][1]);
+    status = q[4][2];
 }
 
 #ifndef DD_ROLL_MIN_WAVES
@@ -709,7 +699,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
     // slot it has just read); otherwise the observation tile
     constexpr int kTileFloats = kSplit ? 4 : kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0);
     __shared__ __attribute__((aligned(16))) float tile[kHeld && !kSplit ? 2 : 1][kTileFloats];
-    __shared__ __attribute__((aligned(16))) f32x4 stage[kSplit ? kBlock / kWave : 1][2][kSplit ? kStageQ<T> : 1]
+    __shared__ __attribute__((aligned(16))) f32x4 stage[kSplit ? kBlock / kWave : 1][2][kSplit ? kStageQ : 1]
                                                       [kSplit ? kWave : 1];
     __shared__ int ctr[2][kBlock / kWave];  // kSplit: produced, consumed
     if constexpr (kSplit) {
@@ -726,16 +716,20 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             char* rew_p = p.reward;
             uint8_t* done_p = p.done;
             const float* obs_f = p.obs + (int64_t)hw0 * DD_OBS_DIM;
+            const bool auto_reset = p.k.c.auto_reset;
+            double total = at(a.total, hi);  // the running total is the writer's (kDefer)
             for (int f = 0; f < p.frames; ++f) {
                 for (int spin = 0; __builtin_amdgcn_readfirstlane(ctr_load(&ctr[0][wv])) <= f && spin < kSpinCap; ++spin)
                     __builtin_amdgcn_s_sleep(1);
                 asm volatile("" ::: "memory");
                 f32x4* slot = &stage[wv][f & 1][0][0];
                 Lane s;
-                T reward;
-                stage_get<T>(slot, lane, s, reward);
+                uint32_t word;
+                stage_get(slot, lane, s, word);
                 asm volatile("" ::: "memory");  // every lane's reads issue before any row write
-                put_out(reinterpret_cast<T*>(rew_p), hi, reward);
+                s.status = word & ~kWasDone;
+                const double reward = finish_deferred<T>(s, (word & kWasDone) != 0, auto_reset, total);
+                put_out(reinterpret_cast<T*>(rew_p), hi, (T)reward);
                 put_out(done_p, hi, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
                 // the rows go where the slot's data was (read above, in order)
                 float* rows = reinterpret_cast<float*>(slot);
@@ -749,6 +743,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
                 rew_p += p.reward_stride;
                 done_p += p.n_total;
             }
+            if (hrow0 + ht < (uint32_t)p.n) at(a.total, hi) = (T)total;
             return;
         }
     }
@@ -854,6 +849,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             __syncwarp();  // frame f - 1's rows (other lanes of this wave) are in LDS
             hold_obs_wave(tile[(f - 1) & 1] + woff, held);
         }
+        DD_COUNT(6);
         const uint32_t act = kActDw ? __builtin_amdgcn_ubfe(slot, act_sh, 3) : slot;
         if constexpr (AFMT == DD_ACT_PHILOX) {
             slot = rollout_action<AFMT>(p, env, f + 2, i, pa);
@@ -868,7 +864,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
         const bool was_done = (s.status & DD_ST_DONE) != 0;
         auto fast = [&]() __attribute__((always_inline)) {
             if constexpr (kParked) return frame_checked_parked<kRef, true, T>(k, sw, act, s, rec);
-            else return frame_checked<kRef, true>(k, sw, act, s);
+            else return frame_checked<kRef, true, kSplit>(k, sw, act, s);  // kSplit: the writer finishes it
         };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
@@ -876,6 +872,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             // to re-spawn takes the one branch
             reward = fast();
             if (__ballot(was_done)) {
+                DD_COUNT(0);
                 if (was_done) {
                     if constexpr (kAhead) ahead.respawn(sw, k.c.max_fuel, env, s);
                     else spawn(sw, k.c.max_fuel, env, s);
@@ -928,7 +925,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
                 consumed = ctr_load(&ctr[1][wv]);
             }
             asm volatile("" ::: "memory");
-            stage_put<T>(&stage[wv][f & 1][0][0], threadIdx.x & (kWave - 1), s, (T)reward);
+            stage_put(&stage[wv][f & 1][0][0], threadIdx.x & (kWave - 1), s, s.status | (was_done ? kWasDone : 0u));
             ctr_store(&ctr[0][wv], f + 1);
         } else {
             put_out(reinterpret_cast<T*>(rew_p), i, (T)reward);
@@ -983,7 +980,8 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
         store_held_wave(held, rsrc_over(obs_prev, slice_bytes));
     }
     if (live) {
-        store_spawn(reload_soa<RolloutArgs, T>(), i, s);  // every field: lanes may have re-spawned
+        // every field (lanes may have re-spawned); kSplit: not the total, the writer's
+        store_spawn<T, !kSplit>(reload_soa<RolloutArgs, T>(), i, s);
         if constexpr (kShaped) { at(p.shaped_hist, i) = h0; at(p.shaped_hist + p.n_total, i) = h1; }
     }
 }
@@ -1380,6 +1378,17 @@ int finish() { return (int)hipGetLastError(); }
 }  // namespace dd
 
 extern "C" {
+
+#ifdef DD_EXP_COUNT
+int dd_lab_counts(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dd::dd_lab_counts), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(dd::dd_lab_counts), z, sizeof(z));
+    }
+    return e;
+}
+#endif
 
 void dd_config_default(DDConfig* c) {
     if (c) *c = dd::reference_config();

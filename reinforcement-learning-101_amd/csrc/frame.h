@@ -234,6 +234,21 @@ __device__ __forceinline__ double measure(Lane& s) {
     return ss;
 }
 
+// Lab-only (-DDD_EXP_COUNT, tools/lab/branch_count_lab.py): how many
+// wave-frames enter each rare branch (one count per wave that enters it).
+#ifdef DD_EXP_COUNT
+static __device__ unsigned long long dd_lab_counts[8];
+#define DD_COUNT(i)                                                                       \
+    do {                                                                                  \
+        const uint64_t m_ = __ballot(1);                                                  \
+        if ((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(m_)) atomicAdd(&dd_lab_counts[i], 1ull); \
+    } while (0)
+#else
+#define DD_COUNT(i) \
+    do {            \
+    } while (0)
+#endif
+
 // DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
 // Platform.reset (platform.py:104-114).  `c` is the call's config (switches,
 // spawn ranges, seed), `max_fuel` the physics' (compile-time under kRef, so
@@ -341,7 +356,10 @@ struct SpawnAhead {
 __device__ __forceinline__ double wrap_angle(double a) {
     double w = a > 180.0 ? a - 360.0 : a;
     w = a < -180.0 ? a + 360.0 : w;
-    if (__builtin_expect(fabs(a) > 540.0, 0)) w = trig::normalize_angle(a);
+    if (__builtin_expect(fabs(a) > 540.0, 0)) {
+        DD_COUNT(4);
+        w = trig::normalize_angle(a);
+    }
     return w;
 }
 
@@ -363,8 +381,16 @@ __device__ __forceinline__ double wrap_angle(double a) {
 // The step kernel (four waves per SIMD) keeps the branches: selects cost it
 // VALU slots the other waves would use.  Only the bottom-centre test near
 // the pad (rare) branches in both.
-template <bool kRef, bool kFlat, bool kExact = false>
+// kDefer (the split rollout's frame waves, reference world, kFlat): the
+// frame stops at the flags and the step count.  Speed, distance, the reward
+// and the running total are left to the writer wave (finish_deferred), which
+// derives them from the frame's state exactly as this function would; the
+// landing test's speed limit compares the squared speed (9 = 3^2: for every
+// squared speed outside the risky edge band, sqrt(ss) > 3 iff ss > 9; NaN
+// fails both).  s.speed, s.dist and s.total are stale on return.
+template <bool kRef, bool kFlat, bool kExact = false, bool kDefer = false>
 __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s, bool* risky_out) {
+    static_assert(!kDefer || (kRef && kFlat && !kExact), "deferred frames: reference world, rollout form");
     const DDConfig& c = k.c;
 
     // apply_thrust: each thruster gated on fuel > 0 at that moment, in order.
@@ -503,7 +529,8 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         }
     }
 
-    const double ss = measure<!kFlat>(s);  // speed (get_speed), distance (physics.distance), shared with get_state
+    // speed (get_speed), distance (physics.distance), shared with get_state
+    const double ss = kDefer ? s.vx * s.vx + s.vy * s.vy : measure<!kFlat>(s);
     const bool upright = fabs(s.angle) <= c.max_landing_angle;
     bool on_pad = false;  // _check_landing: bottom centre on the platform, slow and upright
     const double rx = c.platform_half_width + fabs(c.drone_half_height);
@@ -519,11 +546,13 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     const bool near_pad = upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack;
 #endif
     if (near_pad) {
+        DD_COUNT(2);
         // (lanes out of this reach of the pad: on_pad = false exactly as the
         // reference's comparisons give, the bottom centre lying within
         // |half_height| (+ rounding) of (x, y); NaN fails both tests alike)
         const bool edge = kRef ? fabs(ss - 9.0) <= 0x1p-20 : close(s.speed, c.max_landing_velocity);
-        bool slow = !(s.speed > c.max_landing_velocity);
+        static_assert(reference_config().max_landing_velocity == 3.0, "kDefer's squared speed limit");
+        bool slow = kDefer ? !(ss > 9.0) : !(s.speed > c.max_landing_velocity);
         if constexpr (kExact) {
             if (edge) {  // the reference's speed: sqrt(pow(vx, 2) + pow(vy, 2))
                 double sq = 0.0, v = s.vx;
@@ -538,6 +567,7 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
             risky |= edge;
         }
         if (slow) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
+            DD_COUNT(3);
             double sb, cb;
             sincos_deg<kExact, kSgpr>(s.angle, &sb, &cb);
             const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
@@ -587,6 +617,10 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         term = landing ? c.reward_landing : term;
     }
     s.status |= landing ? (DD_ST_LANDED | DD_ST_DONE) : terminal ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
+    if constexpr (kDefer) {  // (the term above is dead code here)
+        s.steps += 1;
+        return 0.0;
+    }
     const double reward = c.reward_step + term;
     s.total += reward;
     s.steps += 1;
@@ -594,6 +628,30 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
 }
 
 
+
+// The writer wave's half of a kDefer frame: speed and distance of the
+// frame's state (measure()'s arithmetic), then _calculate_reward's value and
+// the running total as frame() + quantize give them (reference world).
+// was_done: the lane started the frame done (auto-reset: re-spawned, reward 0
+// and total 0; sticky: reward 0, total kept).
+template <typename T>
+__device__ __forceinline__ double finish_deferred(Lane& s, bool was_done, bool auto_reset, double& total) {
+    constexpr DDConfig r = reference_config();
+    const double dx = s.px - s.x, dy = s.py - s.y;
+    s.speed = sqrt(s.vx * s.vx + s.vy * s.vy);
+    s.dist = sqrt(dx * dx + dy * dy);
+    if (was_done) {
+        total = auto_reset ? 0.0 : total;
+        return 0.0;
+    }
+    const bool terminal = (s.status & DD_ST_DONE) != 0;
+    const int32_t ti = (s.status & DD_ST_LANDED) ? 100 : s.y > r.ground_level ? -100 : -50;
+    double term = trig::div_exact(r.shaping_offset - s.dist, r.shaping_scale, kRefConsts.inv_shaping);
+    term = terminal ? (double)ti : term;
+    const double reward = r.reward_step + term;
+    total = (double)(T)(total + reward);
+    return reward;
+}
 
 // A frame for kernels that keep the lane's state in registers (the rollout
 // loops): the fast frame, and for a lane it reports risky the frame again
@@ -636,11 +694,11 @@ __device__ __noinline__ void frame_exact_lds(const Consts* kp, const DDConfig* s
 }
 #endif
 
-template <bool kRef, bool kFlat>
+template <bool kRef, bool kFlat, bool kDefer = false>
 __device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
     const Lane s0 = s;
     bool risky = false;
-    double reward = frame<kRef, kFlat>(k, sw, act, s, &risky);
+    double reward = frame<kRef, kFlat, false, kDefer>(k, sw, act, s, &risky);
 #ifdef DD_EXP_RISKY_ONLY
     if (__builtin_expect(__ballot(risky) != 0, 0)) {
         if (risky) reward = __builtin_nan("");
@@ -663,6 +721,7 @@ __device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig&
     }
 #elif !defined(DD_EXP_NO_EXACT)
     if (__builtin_expect(__ballot(risky) != 0, 0)) {
+        DD_COUNT(1);
         if (risky) {
 #ifdef DD_EXP_EXACT_CALL
             const ExactFrame e = frame_exact_call<kRef>(kRef ? nullptr : &k, kRef ? nullptr : &sw, act, s0);

@@ -67,6 +67,7 @@ for v in ${VARIANTS:-base}; do
     vcoef) build vcoef -DDD_EXP_TRIG_VCOEF ;;
     fakespawn) build fakespawn -DDD_EXP_FAKE_SPAWN ;;
     nolicm) build nolicm -mllvm -disable-machine-licm ;;
+    count) build count -DDD_EXP_COUNT ;;
     exactcall) build exactcall -DDD_EXP_EXACT_CALL ;;
     exactlds) build exactlds -DDD_EXP_EXACT_LDS ;;
     riskyonly) build riskyonly -DDD_EXP_RISKY_ONLY ;;
