@@ -227,7 +227,13 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
         const int64_t d = tile * kCols + c;  // this lane's drone (column)
         const bool live = d < p.n;
         float z[K];
+#ifdef DD_EXP_MLP_NOCOMPUTE  // timing-only: the launch, the parameter image and the outputs, no network
+        mid();
+#pragma unroll
+        for (int k = 0; k < K; ++k) z[k] = x[k] + lds[kB4 + k];
+#else
         mlp_body<K, kSplit>(lds, lane, x, z, mid);
+#endif
         if (!live || h != 0) continue;
         emit_outputs<K>(p, d, z);
     }

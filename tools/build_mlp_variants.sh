@@ -18,6 +18,7 @@ for v in ${VARIANTS:-base}; do
   case $v in
     base) build base ;;
     nopair) build nopair -DDD_MLP_PAIR=0 ;;
+    nocompute) build nocompute -DDD_EXP_MLP_NOCOMPUTE ;;
     pv*) build $v -DDD_MLP_PAIR_VALU=${v#pv} ;;
     *) echo "unknown variant $v"; exit 2 ;;
   esac
