@@ -1,7 +1,7 @@
 #!/bin/bash
 # Device assembly of ONE kernel instantiation of csrc/drone_step.hip (seconds,
 # not the library's minutes), then its basic-block / loop counts.
-#   tools/isa_probe.sh OUT.s ['rollout_kernel<float, 0, true, true, false>(RolloutArgs, Soa<float>)'] [-Dflags...]
+#   tools/lab/isa_probe.sh OUT.s ['rollout_kernel<float, 0, true, true, false>(RolloutArgs, Soa<float>)'] [-Dflags...]
 set -e
 OUT=${1:?out.s}
 K=${2:-"rollout_kernel<float, 0, true, true, false>(RolloutArgs, Soa<float>)"}
