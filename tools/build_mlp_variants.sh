@@ -19,6 +19,9 @@ for v in ${VARIANTS:-base}; do
     base) build base ;;
     nopair) build nopair -DDD_MLP_PAIR=0 ;;
     nocompute) build nocompute -DDD_EXP_MLP_NOCOMPUTE ;;
+    maxilp) build maxilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
+    maxocc) build maxocc -mllvm -amdgpu-sched-strategy=max-occupancy ;;
+    itermin) build itermin -mllvm -amdgpu-sched-strategy=iterative-minreg ;;
     pv*) build $v -DDD_MLP_PAIR_VALU=${v#pv} ;;
     *) echo "unknown variant $v"; exit 2 ;;
   esac
