@@ -248,6 +248,23 @@ def test_rollout_switches(cfg, n, precision, gpu_device):
     assert_same_state(roll, loop)
 
 
+@pytest.mark.parametrize("frames", [1, 2, 3])
+def test_split_rollout_few_frames_equal_step_loop(frames, gpu_device):
+    """The split kernel's hand-over at its edges: one, two and three frames
+    (one slot used, both slots, a slot reused), a ragged last block."""
+    n = 4100
+    roll, loop = twins(n, gpu_device, "f32", randomize_drone=True, auto_reset=True, seed=31)
+    warm = torch.randint(0, 8, (40, n), device=gpu_device, dtype=torch.uint8)
+    roll.rollout(warm)
+    loop.rollout(warm)
+    acts = torch.randint(0, 8, (frames, n), device=gpu_device, dtype=torch.uint8)
+    obs, reward, done = roll.rollout(acts)
+    for t in range(frames):
+        o, r, d, _ = loop.step(acts[t])
+        assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
+    assert_same_state(roll, loop)
+
+
 @pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("n", [777, 65_532])
 def test_rollout_short_episodes_equal_step_loop(precision, n, gpu_device):
