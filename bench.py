@@ -324,9 +324,11 @@ def rollout_point(n, frames, precision, seed, dev):
     state = env.step_bytes_per_env(with_obs=False) - 1 - rew.element_size() - 1  # state read + write once
     total = n * frames * fbytes + n * state
     gbs = total / (ms * 1e-3) / 1e9
+    traffic, traffic_note = pmc_traffic_row(n, precision, True, kernel="rollout_kernel", frames=frames)
     out = {"envs": n, "frames": frames, "ms_per_rollout": round(ms, 4),
            "steps_per_s": round(n * frames / (ms * 1e-3), 1), "achieved": round(gbs, 1),
-           "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env_frame": fbytes,
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env_frame": fbytes, "bytes_per_launch": total,
+           "traffic": traffic, "traffic_note": traffic_note,
            "kernel": "dd::rollout_kernel (dd_rollout, one launch per 256-frame rollout)"}
     del env, acts, obs, rew, done
     torch.cuda.empty_cache()
@@ -999,8 +1001,11 @@ def pmc_traffic(n: int, precision: str, obs: bool):
     return pmc_traffic_row(n, precision, obs)[0]
 
 
-def pmc_traffic_row(n: int, precision: str, obs: bool, path: str | None = None):
-    """(bytes or None, note) — the note says why a row was not taken."""
+def pmc_traffic_row(n: int, precision: str, obs: bool, path: str | None = None, kernel: str = "step_kernel",
+                    frames: int | None = None):
+    """(bytes or None, note) — the note says why a row was not taken.  kernel:
+    the row's kernel family (rows without a "kernel" key are step_kernel
+    rows); frames: the rollout rows' frames per launch."""
     from delivery_drone_amd import abi
     path = path or os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -1011,15 +1016,16 @@ def pmc_traffic_row(n: int, precision: str, obs: bool, path: str | None = None):
     have = abi.lib().dd_build_info().decode()
     step_isa = dict(kv.split("=", 1) for kv in have.split(";")).get("step_isa")
     for r in rows.get("rows", []):
-        if r.get("envs") == n and r.get("precision") == precision and r.get("obs") == obs:
+        if (r.get("envs") == n and r.get("precision") == precision and r.get("obs") == obs
+                and r.get("kernel", "step_kernel") == kernel and r.get("frames") == frames):
             got = r.get("build_info")
             if not got:
                 return None, "PMC row has no build_info (measured on an older build)"
             if dict(kv.split("=", 1) for kv in got.split(";")).get("step_isa") != step_isa:
                 return None, f"PMC row measured on step_isa of '{got}', this library is '{have}'"
-            return r.get("hbm_bytes_per_launch"), (f"PMC FETCH_SIZE/WRITE_SIZE passes of the step kernel; its ISA "
+            return r.get("hbm_bytes_per_launch"), (f"PMC FETCH_SIZE/WRITE_SIZE passes of the {kernel}; its ISA "
                                                    f"(step_isa={step_isa}) matches this library's")
-    return None, f"no PMC row for envs={n} precision={precision} obs={obs}"
+    return None, f"no PMC row for {kernel} envs={n} precision={precision} obs={obs} frames={frames}"
 
 
 if __name__ == "__main__":

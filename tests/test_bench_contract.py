@@ -79,6 +79,13 @@ def test_pmc_traffic_only_for_the_measured_build(tmp_path):
     v, note = b.pmc_traffic_row(262144, "f32", True, str(p))
     assert v == 123 and info.split(";")[1] in note  # the note names the matched step ISA
     assert b.pmc_traffic_row(4096, "f32", True, str(p))[0] is None
+    # rollout rows are keyed by kernel and frames, and never stand in for a step row (or the reverse)
+    roll = dict(row, envs=65536, kernel="rollout_kernel", frames=256, hbm_bytes_per_launch=456, build_info=info)
+    p.write_text(json.dumps({"rows": [dict(row, build_info=info), roll]}))
+    assert b.pmc_traffic_row(65536, "f32", True, str(p), kernel="rollout_kernel", frames=256)[0] == 456
+    assert b.pmc_traffic_row(65536, "f32", True, str(p), kernel="rollout_kernel", frames=128)[0] is None
+    assert b.pmc_traffic_row(65536, "f32", True, str(p))[0] is None
+    assert b.pmc_traffic_row(262144, "f32", True, str(p))[0] == 123
 
 
 def _gather_rank(rank, world, port, outdir):
