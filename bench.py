@@ -56,6 +56,9 @@ def parse():
                         "and report it as rollout_point (0 = skip)")
     p.add_argument("--no-extra-points", dest="extra_points", action="store_false",
                    help="skip the notebook-reward point")
+    p.add_argument("--gather-point", action="store_true",
+                   help="initialise the process group and time gather_point even at N=1 (RCCL at world size "
+                        "1 with --dist-backend nccl: the N>1 code path on a one-GPU box)")
     p.add_argument("--hbm-point", type=int, default=16_777_216,
                    help="also time this many drones (HBM-resident) at N=1 and report it as hbm_point (0 = skip)")
     return p.parse_args()
@@ -293,12 +296,22 @@ def hbm_point(n, precision, seed, dev, write_obs, allocs=3, rounds=6):
     return out
 
 
-def rollout_point(n, frames, precision, seed, dev):
+def rollout_point(n, frames, precision, seed, dev, warm=120, timed=40):
     """BASELINE config 5, the PPO rollout shape: n envs x `frames` frames,
     reward + done fused into the step kernel, obs written into a
     [frames, n, 15] rollout buffer — one dd_rollout launch per rollout, actions
     read from a resident [frames, n] buffer.  Bytes per env-frame: action 1 +
-    reward 4 + done 1 + obs 60 (state in/out once per rollout)."""
+    reward 4 + done 1 + obs 60 (state in/out once per rollout).
+
+    Timing: a launch costs a constant ~560k shader cycles, and
+    its time follows the clock the chip holds.  Back-to-back launches see a
+    DVFS transient (GRBM_GUI_ACTIVE per dispatch, profiles/r05/c5_dvfs/): the
+    effective clock falls from ~2.23 to ~1.93 GHz a few launches in and comes
+    back to ~2.28 GHz after ~25 ms of sustained load.  So `warm` untimed
+    launches run first and `timed` launches are timed one by one (HIP events
+    on the launch stream): ms_per_rollout is their median (the steady state);
+    the first launches and the transient's worst are reported beside it."""
+    import statistics
     import torch
     from delivery_drone_amd import EnvConfig, VecDroneEnv
     cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
@@ -309,17 +322,20 @@ def rollout_point(n, frames, precision, seed, dev):
     rew = torch.empty(frames, n, device=dev, dtype=env.float_dtype)
     done = torch.empty(frames, n, device=dev, dtype=torch.bool)
     stream = torch.cuda.Stream(dev)
+    total_launches = warm + timed
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * total_launches)]
     with torch.cuda.stream(stream):
-        env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)  # warm-up
+        env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)  # first launch: code objects, LDS set-up
         torch.cuda.synchronize(dev)
-        reps = 10
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
+        for k in range(total_launches):
+            ev[2 * k].record(stream)
             env.rollout(acts, obs_out=obs, reward_out=rew, done_out=done)
-        e1.record(stream)
+            ev[2 * k + 1].record(stream)
         torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / reps
+    env.check_device_errors()
+    ms_all = [ev[2 * k].elapsed_time(ev[2 * k + 1]) for k in range(total_launches)]
+    steady = ms_all[warm:]
+    ms = statistics.median(steady)
     fbytes = 1 + rew.element_size() + 1 + 60
     state = env.step_bytes_per_env(with_obs=False) - 1 - rew.element_size() - 1  # state read + write once
     total = n * frames * fbytes + n * state
@@ -328,6 +344,12 @@ def rollout_point(n, frames, precision, seed, dev):
     out = {"envs": n, "frames": frames, "ms_per_rollout": round(ms, 4),
            "steps_per_s": round(n * frames / (ms * 1e-3), 1), "achieved": round(gbs, 1),
            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env_frame": fbytes, "bytes_per_launch": total,
+           "timing": {"warm_launches": warm, "timed_launches": timed,
+                      "ms_steady_median": round(ms, 4), "ms_steady_mean": round(statistics.mean(steady), 4),
+                      "ms_first5_median": round(statistics.median(ms_all[:5]), 4),
+                      "ms_transient_max": round(max(ms_all[:warm]), 4),
+                      "rule": "median of the timed launches after the warm ones (DVFS transient excluded)"},
+           "kernel_choice": env.last_rollout_kernel,
            "traffic": traffic, "traffic_note": traffic_note,
            "kernel": "dd::rollout_kernel (dd_rollout, one launch per 256-frame rollout)"}
     del env, acts, obs, rew, done
@@ -546,23 +568,26 @@ def gae_point(n, frames, dev):
             "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes": nbytes, "kernel": "dd::gae_kernel"}
 
 
-def notebook_point(n, precision, seed, dev):
-    """The step with the notebooks' reward fused:
-    reward_mode='notebook', max_steps=300, config-3 batch."""
+def notebook_point(n, precision, seed, dev, mode="notebook"):
+    """The step with a notebook's reward fused:
+    reward_mode='notebook' (PPO's calc_reward with its two-frame history) or
+    'reinforce' (Policy_Gradients.ipynb's), max_steps=300, config-3 batch."""
     import torch
     from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
     cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=seed)
-    env = VecDroneEnv(n, device=dev, config=cfg, precision=precision, reward_mode="notebook", max_steps=300)
+    env = VecDroneEnv(n, device=dev, config=cfg, precision=precision, reward_mode=mode, max_steps=300)
     env.reset()
     rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
     ms = time_steps(env, rows, 500, 50, torch.cuda.Stream(dev))
-    bpe = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=True) + 8 + 8 + 4 + 1  # + hist r/w, shaped r, done
+    fb = 4 if precision == "f32" else 8
+    # + shaped reward and done; PPO also reads and writes its f64 history slot
+    bpe = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=True) + fb + 1 + (16 if mode == "notebook" else 0)
     gbs = bpe * n / (ms * 1e-3) / 1e9
     del env, rows
     torch.cuda.empty_cache()
     return {"envs": n, "us_per_step": round(ms * 1e3, 3), "steps_per_s": round(n / (ms * 1e-3), 1),
             "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env": bpe,
-            "kernel": "dd::step_kernel<float, 0, true, true> (reward_mode='notebook')"}
+            "kernel": f"dd::step_kernel<float, 0, true, {1 if mode == 'notebook' else 2}> (reward_mode='{mode}')"}
 
 
 MLP_FLOPS_PER_ROW = 2 * (15 * 128 + 128 * 128 + 128 * 64 + 64 * 3)  # the notebooks' actor, algorithmic
@@ -813,7 +838,11 @@ def main():
     local_dev = local % max(ndev, 1)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    use_pg = world > 1 or args.gather_point
+    if use_pg:
+        if "MASTER_ADDR" not in os.environ:  # --gather-point outside torch.distributed.run
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29531"),
+                              RANK="0", WORLD_SIZE="1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -896,12 +925,12 @@ def main():
     if world == 1 and args.hbm_point > 0:
         hbm = hbm_point(args.hbm_point, args.precision, args.seed, dev, write_obs)
     gp = None
-    if world > 1:
+    if use_pg:
         try:  # an optional extra: a failure here must not cost the step measurement
             gp = gather_point(env.obs, n, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
             gp = {"error": f"{type(e).__name__}: {e}"[:300]}
-    c5 = c5a = g5 = c2 = nb = f64p = ppp = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None
+    c5 = c5a = g5 = c2 = nb = rf = f64p = ppp = pp = pr = pp16 = pr16 = pf = pf16 = sp = rp = None
     if world == 1 and args.rollout_point > 0:
         c5 = rollout_point(args.rollout_point, 256, args.precision, args.seed, dev)
         c5a = step_loop_point(args.rollout_point, 256, args.precision, args.seed, dev)
@@ -909,6 +938,7 @@ def main():
     if world == 1 and args.extra_points:
         c2 = config2_point(args.seed, dev)
         nb = notebook_point(n, args.precision, args.seed, dev)
+        rf = notebook_point(n, args.precision, args.seed, dev, "reinforce")
         f64p = f64_point(n, args.seed, dev)
         ppp = ping_pong_point(n, args.seed, dev)
         pp = policy_point(args.rollout_point or 65_536, args.seed, dev)
@@ -974,6 +1004,7 @@ def main():
             "gather_point": gp,
             "gae_point": g5,
             "notebook_reward_point": nb,
+            "reinforce_reward_point": rf,
             "f64_point": f64p,
             "ping_pong_point": ppp,
             "policy_point": pp,
@@ -989,7 +1020,7 @@ def main():
             "build_info": abi.lib().dd_build_info().decode(),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

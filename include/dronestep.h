@@ -14,6 +14,8 @@
  * and for the notebooks' side of the loop:
  *
  *   calc_reward + max_steps  Actor_Critic_PPO.ipynb:164-263, :886-888 -> dd_step (shaped_*)
+ *   calc_reward + max_steps  Policy_Gradients.ipynb:162-238, :590-593 (REINFORCE)
+ *                                                       -> dd_step (shaped_mode)
  *   the collection loop       Actor_Critic_PPO.ipynb:797-917          -> dd_rollout
  *   DroneGamerBoi / DroneTeacherBoi + Bernoulli.sample / log_prob
  *                             Actor_Critic_PPO.ipynb:376-424, :851-859 -> dd_mlp_forward
@@ -47,7 +49,8 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 10 /* 10: DDStepIO.state_out (ping-pong state); 9: packed MLP buffers carry a layout tag */
+#define DD_ABI_VERSION 11 /* 11: shaped_mode (REINFORCE reward), DDRolloutIO.kernel, dd_rollout_kernel,
+                              dd_device_errors; 10: DDStepIO.state_out (ping-pong state) */
 
 /* Storage precision of the SoA floating-point fields. */
 enum { DD_F32 = 0, DD_F64 = 1 };
@@ -73,6 +76,17 @@ enum {
     DD_ST_CRASHED = 1u << 2, /* Drone.crashed                     */
     DD_ST_PLAT_LEFT = 1u << 3 /* Platform.direction == -1 (moving) */
 };
+
+/* The notebooks' shaped reward (DDStepIO / DDRolloutIO / DDPolicyRolloutIO
+ * shaped_mode), each with its collection loop's max_steps timeout (done, -500
+ * unless landed):
+ *   DD_SHAPED_PPO        calc_reward(state, prev_state) of Actor_Critic_PPO.ipynb:
+ *                        164-263 (also Actor_Critic_Basic), prev_state two frames
+ *                        back as collect_episodes_ppo passes it; needs shaped_hist.
+ *   DD_SHAPED_REINFORCE  calc_reward(state) of Policy_Gradients.ipynb:162-238
+ *                        (distance-scaled time penalty, terminal 500 + fuel * 100
+ *                        or -200 / -300), timeout :590-593; no history. */
+enum { DD_SHAPED_PPO = 0, DD_SHAPED_REINFORCE = 1 };
 
 /* Width of one observation row: state_to_array order of
  * Actor_Critic_PPO.ipynb:346-366 (x, y, vx, vy, angle, omega, fuel, px, py,
@@ -177,7 +191,9 @@ typedef struct DDStepIO {
     void *shaped_reward;  /* float or double [N] by precision                   */
     uint8_t *shaped_done; /* uint8 [N]: done or truncated                        */
     int32_t max_steps;    /* <= 0: no truncation                                 */
-    int32_t _pad2;
+    int32_t shaped_mode;  /* DD_SHAPED_PPO (the three pointers above, or none) or
+                             DD_SHAPED_REINFORCE (shaped_reward and shaped_done
+                             required, shaped_hist not read)                     */
     /* Ping-pong state (nullable = in place): the step reads the nine fields
      * that change every frame (x y vx vy angle omega fuel total_reward steps)
      * from `st` and writes them to *state_out's arrays, which must not alias
@@ -202,16 +218,29 @@ typedef struct DDRolloutIO {
     float *obs;           /* float [frames][N][15] (nullable)                   */
     uint64_t action_seed; /* DD_ACT_PHILOX key                                  */
     int64_t action_step;  /* DD_ACT_PHILOX counter of frame 0 (frame k: +k)     */
-    /* Notebook reward mode (as DDStepIO's shaped_*; NULL = engine reward):
-     * reward / done then receive calc_reward (Actor_Critic_PPO.ipynb:164-263)
-     * and the notebook's done with the max_steps timeout (:886-888), and the
-     * [2][N] history is read at launch and written back at its end.          */
+    /* Notebook reward mode (as DDStepIO's shaped_*): with shaped_mode
+     * DD_SHAPED_PPO and shaped_hist set, or DD_SHAPED_REINFORCE, reward / done
+     * receive the notebook's calc_reward and done with the max_steps timeout,
+     * and the PPO [2][N] history is read at launch and written back at its end.
+     * DD_SHAPED_PPO with shaped_hist NULL = the engine reward.              */
     double *shaped_hist;  /* double [2][N] (nullable)                           */
     void *engine_reward;  /* shaped mode: the engine's reward [frames][N] (nullable) */
     uint8_t *engine_done; /* and done; both or neither                          */
     int32_t max_steps;    /* shaped mode: episode cap, <= 0 = none              */
-    int32_t reserved;
+    int32_t shaped_mode;  /* DD_SHAPED_*                                        */
+    int32_t kernel;       /* DD_ROLLOUT_AUTO / _SINGLE / _SPLIT_NO_WAIT          */
+    int32_t _pad;
 } DDRolloutIO;
+
+/* DDRolloutIO.kernel.  AUTO: the split kernel (frame waves + writer waves,
+ * DESIGN.md §4) where it applies (reference world, engine reward, obs rows,
+ * one block per CU or fewer), the single-role kernel elsewhere.  SINGLE: never
+ * the split kernel.  SPLIT_NO_WAIT (diagnostic): as AUTO with the split
+ * kernel's hand-over waits capped at zero polls, which reports DD_ERR_HANDOVER
+ * through dd_device_errors — the check that a broken hand-over is not silent. */
+enum { DD_ROLLOUT_AUTO = 0, DD_ROLLOUT_SINGLE = 1, DD_ROLLOUT_SPLIT_NO_WAIT = 2 };
+/* dd_rollout_kernel(): the kernel a dd_rollout call launches (its first chunk). */
+enum { DD_ROLLOUT_FLUSHED = 16, DD_ROLLOUT_HELD = 17, DD_ROLLOUT_SPLIT = 18 };
 
 /* Fills *cfg with config.py's values (randomize_platform = 1, others 0). */
 void dd_config_default(DDConfig *cfg);
@@ -225,6 +254,17 @@ int dd_step(const DDConfig *cfg, const DDState *st, const DDStepIO *io,
  * same frame as dd_step, game_engine.py:95-138, applied frames times. */
 int dd_rollout(const DDConfig *cfg, const DDState *st, const DDRolloutIO *io,
                int64_t n, void *stream);
+
+/* Which kernel dd_rollout takes for these arguments (DD_ROLLOUT_FLUSHED /
+ * _HELD / _SPLIT), -1 for invalid ones.  No GPU work. */
+int dd_rollout_kernel(const DDConfig *cfg, const DDState *st, const DDRolloutIO *io,
+                      int64_t n);
+
+/* Sticky error bits the kernels set on the device (DD_ERR_*), read
+ * synchronously (the device is synchronised) and cleared if `clear`. */
+enum { DD_ERR_HANDOVER = 1 }; /* a split-rollout hand-over wait ran out: rows of
+                                 that launch are not to be trusted */
+int dd_device_errors(uint32_t *bits, int32_t clear);
 
 /* Re-spawn lanes (DroneGame.reset, game_engine.py:59-93).  mask: uint8 [N],
  * nonzero = reset that lane; NULL = all lanes.  obs (nullable) receives the
@@ -353,6 +393,8 @@ typedef struct DDPolicyRolloutIO {
     double *shaped_hist;  /* notebook reward mode, as DDRolloutIO (nullable)    */
     void *engine_reward;  /* notebook mode: the engine's reward / done          */
     uint8_t *engine_done; /* [frames][N] (both or neither, nullable)            */
+    int32_t shaped_mode;  /* DD_SHAPED_* as DDRolloutIO                         */
+    int32_t _pad;
 } DDPolicyRolloutIO;
 
 int dd_policy_rollout(const DDConfig *cfg, const DDState *st, const float *packed,

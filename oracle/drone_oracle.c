@@ -36,6 +36,7 @@
 static double (*volatile ora_pow)(double, double) = pow;
 static double (*volatile ora_sin)(double) = sin;
 static double (*volatile ora_cos)(double) = cos;
+static double (*volatile ora_exp)(double) = exp;
 
 #define ORA_PI 3.141592653589793238462643383279502884
 
@@ -260,6 +261,55 @@ double ora_notebook_reward(const double o[DD_OBS_DIM], double prev_dist) {
     return total;
 }
 
+/* calc_reward(state)['total'] of the REINFORCE notebook, Policy_Gradients.ipynb:
+ * 162-238, with calc_velocity_alignment (:128-153) and rl_helpers/scalers.py's
+ * inverse_quadratic / scaled_shifted_negative_sigmoid, as its Python
+ * evaluates them (`x**2` = pow(x, 2), math.exp = exp, int * float products). */
+double ora_reinforce_reward(const double o[DD_OBS_DIM]) {
+    double vx = o[2], vy = o[3], angle = o[4], fuel = o[6], dist = o[9], dx = o[10], dy = o[11], speed = o[12];
+    int landed = o[13] != 0.0, crashed = o[14] != 0.0;
+    double total = 0;
+    /* -inverse_quadratic(dist, decay=50, scaler=1 - 0.3) - 0.3 */
+    double time_penalty = -((1 - 0.3) * (1 / (1 + (50 * ora_pow(dist, 2))))) - 0.3;
+    total += time_penalty;
+    double odx = -dx, ody = -dy, align;
+    double onorm = sqrt(ora_pow(odx, 2) + ora_pow(ody, 2));
+    if (onorm < 1e-6) {
+        align = 1.0;
+    } else {
+        odx /= onorm;
+        ody /= onorm;
+        if (speed < 1e-6) {
+            align = 0.0;
+        } else {
+            double vdx = vx / speed, vdy = vy / speed;
+            align = vdx * odx + vdy * ody;
+        }
+    }
+    double distance = 0, valign = 0;
+    if (dist > 0.065 && dy > 0) {
+        double sig = 4.5 * (1 / (1 + ora_exp(10 * (dist - 0.5))));
+        distance = (double)(align > 0) * speed * sig;
+        if (align > 0) valign = 0.5;
+    }
+    total += distance;
+    total += valign;
+    double excess = fabs(angle) - (((0.20 - 0.111) * dist) + 0.111);
+    total += -(excess > 0 ? excess : 0);
+    if (dist < 1) total += -2 * ((speed - 0.1) > 0 ? speed - 0.1 : 0);
+    else total += -1 * ((speed - 0.4) > 0 ? speed - 0.4 : 0);
+    if (!(dy > 0)) total += dy * 4.0;
+    double terminal = 0;
+    if (landed) {
+        terminal = 500.0 + fuel * 100.0;
+    } else if (crashed) {
+        terminal = -200.0;
+        if (dist > 0.3) terminal -= 100.0;
+    }
+    total += terminal;
+    return total;
+}
+
 /* ---- SoA batch entry points (host arrays, DDState layout) ----------------*/
 #define FLD(name) (st->precision == DD_F64 ? ((double *)st->name)[i] : (double)((float *)st->name)[i])
 #define PUT(name, v)                                                \
@@ -297,13 +347,14 @@ static void emit_obs(const DDConfig *c, const OraLane *s, int64_t i, float *obs,
 }
 
 /* dd_step semantics over host arrays; actions are DD_ACT_BITMASK bytes.
- * reward is float or double by st->precision.  hist/shaped/shaped_done
- * (all or none) add the notebooks' reward: hist is [2][n] doubles, slot
- * steps & 1 holds the distance of the state two frames back (NaN = None),
- * max_steps > 0 adds collect_episodes_ppo's timeout. */
+ * reward is float or double by st->precision.  shaped/shaped_done add the
+ * notebooks' reward: mode DD_SHAPED_PPO with hist ([2][n] doubles, slot
+ * steps & 1 holds the distance of the state two frames back, NaN = None),
+ * DD_SHAPED_REINFORCE without; max_steps > 0 adds the collection loops'
+ * timeout. */
 int ora_step_shaped(const DDConfig *c, const DDState *st, const uint8_t *actions, void *reward, uint8_t *done,
                     float *obs, double *obs64, double *hist, void *shaped, uint8_t *shaped_done,
-                    int32_t max_steps, int64_t n) {
+                    int32_t max_steps, int32_t mode, int64_t n) {
     for (int64_t i = 0; i < n; ++i) {
         OraLane s;
         load_lane(st, i, &s);
@@ -312,7 +363,7 @@ int ora_step_shaped(const DDConfig *c, const DDState *st, const uint8_t *actions
         if (s.status & DD_ST_DONE) {
             if (c->auto_reset) {
                 ora_spawn(c, st->env_id_base + i, &s);
-                if (hist) {
+                if (hist && mode == DD_SHAPED_PPO) {
                     hist[i] = dist2d(s.x, s.y, s.px, s.py) / c->world_width;
                     hist[n + i] = NAN;
                 }
@@ -321,12 +372,16 @@ int ora_step_shaped(const DDConfig *c, const DDState *st, const uint8_t *actions
             }
         } else {
             r = ora_frame(c, actions[i], &s);
-            if (hist) {
+            if (shaped) {
                 double o[DD_OBS_DIM];
                 ora_observe(c, &s, o);
-                double *slot = hist + (s.steps & 1) * n;
-                sr = ora_notebook_reward(o, slot[i]);
-                slot[i] = o[9];
+                if (mode == DD_SHAPED_REINFORCE) {
+                    sr = ora_reinforce_reward(o);
+                } else {
+                    double *slot = hist + (s.steps & 1) * n;
+                    sr = ora_notebook_reward(o, slot[i]);
+                    slot[i] = o[9];
+                }
                 sd = (s.status & DD_ST_DONE) != 0;
                 if (max_steps > 0 && s.steps >= max_steps) {
                     if (!(s.status & DD_ST_LANDED)) sr -= 500;
@@ -339,7 +394,7 @@ int ora_step_shaped(const DDConfig *c, const DDState *st, const uint8_t *actions
         if (st->precision == DD_F64) ((double *)reward)[i] = r;
         else ((float *)reward)[i] = (float)r;
         done[i] = (s.status & DD_ST_DONE) ? 1 : 0;
-        if (hist) {
+        if (shaped) {
             if (st->precision == DD_F64) ((double *)shaped)[i] = sr;
             else ((float *)shaped)[i] = (float)sr;
             shaped_done[i] = (uint8_t)sd;
@@ -351,7 +406,7 @@ int ora_step_shaped(const DDConfig *c, const DDState *st, const uint8_t *actions
 
 int ora_step(const DDConfig *c, const DDState *st, const uint8_t *actions, void *reward, uint8_t *done,
              float *obs, double *obs64, int64_t n) {
-    return ora_step_shaped(c, st, actions, reward, done, obs, obs64, NULL, NULL, NULL, 0, n);
+    return ora_step_shaped(c, st, actions, reward, done, obs, obs64, NULL, NULL, NULL, 0, DD_SHAPED_PPO, n);
 }
 
 /* Threshold probing (tests/threshold_states.py): the post-update quantities

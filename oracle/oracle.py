@@ -47,9 +47,12 @@ def lib() -> ctypes.CDLL:
                 P = ctypes.c_void_p
                 cfgp, stp = ctypes.POINTER(abi.DDConfig), ctypes.POINTER(abi.DDState)
                 h.ora_step.argtypes = [cfgp, stp, P, P, P, P, P, ctypes.c_int64]
-                h.ora_step_shaped.argtypes = [cfgp, stp, P, P, P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int64]
+                h.ora_step_shaped.argtypes = [cfgp, stp, P, P, P, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32,
+                                              ctypes.c_int64]
                 h.ora_notebook_reward.argtypes = [P, ctypes.c_double]
                 h.ora_notebook_reward.restype = ctypes.c_double
+                h.ora_reinforce_reward.argtypes = [P]
+                h.ora_reinforce_reward.restype = ctypes.c_double
                 h.ora_reset.argtypes = [cfgp, stp, P, P, P, ctypes.c_int64]
                 h.ora_write_obs.argtypes = [cfgp, stp, P, P, ctypes.c_int64]
                 h.ora_get_info.argtypes = [cfgp, stp, P, P, ctypes.c_int64]
@@ -124,11 +127,14 @@ class OracleEnv:
                        _p(obs64), self.n)
         return obs, reward, done.astype(bool), obs64
 
-    def step_shaped(self, actions, hist, max_steps=0):
-        """step() plus the notebooks' reward; `hist` is a [2, n] float64 array
-        updated in place.  Returns obs, reward, done, obs64, shaped, shaped_done."""
+    def step_shaped(self, actions, hist, max_steps=0, mode="notebook"):
+        """step() plus the notebooks' reward: PPO's (``mode="notebook"``;
+        `hist` is a [2, n] float64 array updated in place) or REINFORCE's
+        (``mode="reinforce"``; `hist` is not read).  Returns obs, reward, done,
+        obs64, shaped, shaped_done."""
         a = bitmask(actions)
-        assert hist.shape == (2, self.n) and hist.dtype == np.float64 and hist.flags.c_contiguous
+        if mode == "notebook" or hist is not None:
+            assert hist.shape == (2, self.n) and hist.dtype == np.float64 and hist.flags.c_contiguous
         reward = np.zeros(self.n, dtype=self.dtype)
         shaped = np.zeros(self.n, dtype=self.dtype)
         done = np.zeros(self.n, dtype=np.uint8)
@@ -137,7 +143,8 @@ class OracleEnv:
         obs64 = np.zeros((self.n, 15), dtype=np.float64)
         st = self._state()
         lib().ora_step_shaped(ctypes.byref(self._cfg), ctypes.byref(st), _p(a), _p(reward), _p(done), _p(obs),
-                              _p(obs64), _p(hist), _p(shaped), _p(sdone), int(max_steps), self.n)
+                              _p(obs64), _p(hist) if hist is not None else None, _p(shaped), _p(sdone),
+                              int(max_steps), 1 if mode == "reinforce" else 0, self.n)
         return obs, reward, done.astype(bool), obs64, shaped, sdone.astype(bool)
 
     def reset(self, mask=None):

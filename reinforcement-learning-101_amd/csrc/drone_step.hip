@@ -41,80 +41,26 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // lane, so every load/store is `global_load_dword v, v_off, s[base]`.
 // ---------------------------------------------------------------------------
 
-// Store cache policies (gfx950): kPlain = write-back into the XCD's L2 (dirty
-// lines leave at the kernel-end release); kNT = non-temporal hint (still
-// write-back); kWT = sc1, write-through (the bytes leave L2 as the wave
-// stores them, nothing is left dirty for the kernel boundary); kWTNT = both.
-enum StorePolicy { kPlain = 0, kWT = 1, kNT = 2, kWTNT = 3 };
-#ifndef DD_ST_STATE
-#define DD_ST_STATE kPlain  // SoA state fields
-#endif
-#ifndef DD_ST_OUT
-#define DD_ST_OUT kNT  // reward / done streams
-#endif
-#ifndef DD_ST_OBS
-#define DD_ST_OBS kNT  // observation rows (16-byte stores)
-#endif
-
-// A buffer resource over [p, p + 2 GiB): raw buffer stores carry any cache
-// policy (aux: bit1 nt, bit4 sc1).  Word 3 is gfx9's 32-bit data format.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+// Store cache policies (gfx950), measured per stream: the
+// SoA state is stored plainly (write-back into the XCD's L2; the next step
+// reads it there), the output streams this kernel never re-reads (reward,
+// done, observation rows) with the non-temporal hint (+2-6 % at 262,144 and
+// 16.8M lanes).  Write-through (sc1) state stores made the next step's loads
+// miss L2 (0.5 -> 1.35 us), non-temporal state stores / loads were slower.
+template <typename E>
+__device__ __forceinline__ void store_nt(E* base, uint32_t i, E v) {
+    __builtin_nontemporal_store(v, &at(base, i));
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-template <int P, typename E>
-__device__ __forceinline__ void store_as(E* base, uint32_t i, E v) {
-    if constexpr (P >= 100) {  // lab sweeps: a raw buffer store with cache-policy bits P - 100
-        const uint32_t off = i * (uint32_t)sizeof(E);
-        if constexpr (sizeof(E) == 1)
-            __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), rsrc_of(base), off, 0, P - 100);
-        else if constexpr (sizeof(E) == 4)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rsrc_of(base), off, 0, P - 100);
-        else
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsrc_of(base), off, 0, P - 100);
-    } else if constexpr (P == kPlain) {
-        at(base, i) = v;
-    } else if constexpr (P == kNT) {
-        __builtin_nontemporal_store(v, &at(base, i));
-    } else if constexpr (P == kWT) {
-        __hip_atomic_store(&at(base, i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        const uint32_t off = i * (uint32_t)sizeof(E);
-        if constexpr (sizeof(E) == 1)
-            __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), rsrc_of(base), off, 0, 18);
-        else if constexpr (sizeof(E) == 4)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rsrc_of(base), off, 0, 18);
-        else
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsrc_of(base), off, 0, 18);
-    }
-}
-
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// One 16-byte observation store at float4 index k of a wave-uniform base.
-template <int P>
-__device__ __forceinline__ void store_obs4(f32x4* base, uint32_t k, f32x4 v) {
-    if constexpr (P >= 100) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base), k * 16u, 0, P - 100);
-    } else if constexpr (P == kPlain) {
-        at(base, k) = v;
-    } else if constexpr (P == kNT) {
-        __builtin_nontemporal_store(v, &at(base, k));
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base), k * 16u, 0,
-                                               P == kWT ? 16 : 18);
-    }
-}
-
 // Output streams this kernel never re-reads (reward, done) are stored
-// non-temporally, like the obs tile (+2-3 % at 262k and 16M lanes, lab3);
-// DD_ST_OUT selects another policy for A/B runs.
+// non-temporally, like the obs tile.
 template <typename E>
 __device__ __forceinline__ void put_out(E* base, uint32_t i, E v) {
     asm volatile("" : "+v"(i));  // keep the offset 32-bit and local: SGPR-base store
-    store_as<DD_ST_OUT>(base, i, v);
+    store_nt(base, i, v);
 }
 
 template <typename T>
@@ -126,7 +72,7 @@ __device__ __forceinline__ void load_dynamics(const Soa<T>& a, uint32_t i, Lane&
 
 template <typename E>
 __device__ __forceinline__ void put_state(E* base, uint32_t i, E v) {
-    store_as<DD_ST_STATE>(base, i, v);
+    at(base, i) = v;
 }
 
 template <typename T>
@@ -157,13 +103,7 @@ __device__ __forceinline__ void flush_obs_tile(const float* tile, float* dst, in
         const int nv = nf >> 2;
         const f32x4* src4 = reinterpret_cast<const f32x4*>(tile);
         f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
-        for (int k = threadIdx.x; k < nv; k += NB) {
-#ifdef DD_PLAIN_OBS_STORES
-            dst4[k] = src4[k];
-#else
-            __builtin_nontemporal_store(src4[k], &dst4[k]);
-#endif
-        }
+        for (int k = threadIdx.x; k < nv; k += NB) __builtin_nontemporal_store(src4[k], &dst4[k]);
         for (int k = (nv << 2) + threadIdx.x; k < nf; k += NB) dst[k] = tile[k];
     } else {
         for (int k = threadIdx.x; k < nf; k += NB) dst[k] = tile[k];
@@ -183,7 +123,7 @@ __device__ __forceinline__ void flush_obs_wave(const float* wtile, float* dst, i
         const int nv = nf >> 2;
         const f32x4* src4 = reinterpret_cast<const f32x4*>(wtile);
         f32x4* dst4 = reinterpret_cast<f32x4*>(uniform_ptr(dst));
-        for (int k = lane; k < nv; k += kWave) store_obs4<DD_ST_OBS>(dst4, (uint32_t)k, src4[k]);
+        for (int k = lane; k < nv; k += kWave) store_nt(dst4, (uint32_t)k, src4[k]);
         for (int k = (nv << 2) + lane; k < nf; k += kWave) dst[k] = wtile[k];
     } else {
         for (int k = lane; k < nf; k += kWave) dst[k] = wtile[k];
@@ -222,16 +162,11 @@ struct StepArgs {
     void* shaped_reward;
     uint8_t* shaped_done;
     int32_t max_steps;
-    int32_t ping_pong;     // DDStepIO.state_out set: the kernel's `o` is not `a`
 };
 
-#ifndef DD_STEP_MIN_WAVES
-#define DD_STEP_MIN_WAVES 1  // per SIMD; experiments raise it to force fewer VGPRs
-#endif
-#ifndef DD_STEP_BLOCK
-#define DD_STEP_BLOCK 256  // lanes (= drones) per step block; experiments try 512 / 1024
-#endif
-constexpr int kStepBlock = DD_STEP_BLOCK;
+// 256 lanes per block: 128 / 512 / 1024 measured +0 / +4 / +14 % at 262,144
+// drones; no occupancy floor (forcing 8 waves per SIMD spilled).
+constexpr int kStepBlock = 256;
 
 // A lane's inputs as loaded (storage width), before widening to double.
 template <typename T>
@@ -243,22 +178,16 @@ struct Raw {
 
 template <typename T, int AFMT>
 __device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, uint32_t i, Raw<T>& r) {
-#ifndef DD_EXP_LATE_ACT
     // The action is loaded first and pinned below: only the live branch reads
     // it, and left to itself the compiler sank its load into that branch,
     // i.e. behind the wait for the status byte: a second memory round trip.
     r.act = load_action<AFMT>(actions, i);
-#endif
     r.x = at(a.x, i); r.y = at(a.y, i); r.vx = at(a.vx, i); r.vy = at(a.vy, i);
     r.angle = at(a.angle, i); r.omega = at(a.omega, i); r.fuel = at(a.fuel, i);
     r.px = at(a.px, i); r.py = at(a.py, i); r.total = at(a.total, i);
     r.status = at(a.status, i);
     r.steps = at(a.steps, i);
-#ifdef DD_EXP_LATE_ACT
-    r.act = load_action<AFMT>(actions, i);
-#else
     asm volatile("" ::"v"(r.act));  // every load is issued; this waits for the oldest only
-#endif
 }
 
 // Everything after the loads for one lane: the frame (or sticky done / auto
@@ -266,10 +195,11 @@ __device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, u
 // (LDS).  Returns whether the lane's episode ended in this call.  The fast
 // frame (kExact false) may report the lane risky (frame.h): then nothing is
 // stored, and the kernel calls finish_lane again with kExact.
-// `o`: where the nine per-frame fields go (x y vx vy angle omega fuel total
-// steps): `a` itself in place, the ping-pong arrays with DDStepIO.state_out
-// (px, py, status and episode always go to `a`).
-template <typename T, bool kRef, bool kShaped, bool kExact = false>
+// kShape: the notebooks' reward fused (frame.h, kShapePpo / kShapeReinforce).
+// kPP (ping-pong, DDStepIO.state_out): the nine per-frame fields (x y vx vy
+// angle omega fuel total steps) go to `o`; px, py, status and episode always
+// go to `a`.  In place (the usual case) the kernel has no `o` at all.
+template <typename T, bool kRef, int kShape, bool kPP, bool kExact = false>
 __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, const Soa<T>& o, uint32_t i,
                                             const Raw<T>& r, float* orow, bool* risky = nullptr) {
     const DDConfig& sw = p.k.c;
@@ -290,7 +220,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
             s.episode = at(a.episode, i);
             spawn(sw, k.c.max_fuel, a.env_id_base + i, s);
             respawned = true;
-            if constexpr (kShaped) {  // the notebook's history restarts: prev_state None
+            if constexpr (kShape == kShapePpo) {  // the notebook's history restarts: prev_state None
                 at(p.shaped_hist, i) = trig::div_exact(s.dist, k.c.world_width, k.inv_w);
                 at(p.shaped_hist + p.hist_stride, i) = __builtin_nan("");
             }
@@ -299,12 +229,6 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
             shaped_done = true;
         }
     } else {
-#ifdef DD_EXP_NOMATH  // timing-only: same loads/stores, trivial arithmetic
-        s.x += s.vx; s.y += s.vy; s.angle += s.omega; s.fuel -= (double)r.act; s.steps += 1;
-        s.speed = s.vx; s.dist = s.vy;
-        reward = s.x;
-        s.status |= (s.y > 550.0) ? (DD_ST_CRASHED | DD_ST_DONE) : 0u;
-#else
         bool rk = false;
         reward = frame<kRef, false, kExact>(k, sw, r.act, s, &rk);
         if constexpr (!kExact) {
@@ -313,15 +237,18 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
                 return false;
             }
         }
-#endif
-        if constexpr (kShaped) {
+        if constexpr (kShape != kShapeNone) {
             double v[13];
             observe_values<false, true>(k, s, v);  // the notebook reward's doubles: exact quotients
-            double* slot = p.shaped_hist + (s.steps & 1) * p.hist_stride;  // two frames back
-            shaped = notebook_reward(v, s.status, at(slot, i));
-            at(slot, i) = v[9];
+            if constexpr (kShape == kShapePpo) {
+                double* slot = p.shaped_hist + (s.steps & 1) * p.hist_stride;  // two frames back
+                shaped = notebook_reward(v, s.status, at(slot, i));
+                at(slot, i) = v[9];
+            } else {
+                shaped = reinforce_reward(v, s.status);
+            }
             shaped_done = (s.status & DD_ST_DONE) != 0;
-            if (p.max_steps > 0 && s.steps >= p.max_steps) {  // collect_episodes_ppo timeout
+            if (p.max_steps > 0 && s.steps >= p.max_steps) {  // the collection loops' timeout
                 shaped = (s.status & DD_ST_LANDED) ? shaped : shaped - 500;
                 shaped_done = true;
                 s.status |= DD_ST_DONE;  // the episode ends here (TimeLimit)
@@ -336,7 +263,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     // writes nothing; status and px only change on the terminal frame, a
     // respawn or a moving platform; py and episode only on a respawn.
     // (with separate out arrays a sticky lane copies its fields across)
-    const bool sticky = (r.status & DD_ST_DONE) && !respawned && !p.ping_pong;
+    const bool sticky = (r.status & DD_ST_DONE) && !respawned && !kPP;
     if (!sticky) {
         uint32_t j = i;
         asm volatile("" : "+v"(j));  // an offset defined in this block: isel folds it into saddr stores
@@ -350,7 +277,7 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     }
     put_out(static_cast<T*>(p.reward), i, (T)reward);
     put_out(p.done, i, (uint8_t)((s.status & DD_ST_DONE) ? 1 : 0));
-    if constexpr (kShaped) {
+    if constexpr (kShape != kShapeNone) {
         put_out(static_cast<T*>(p.shaped_reward), i, (T)shaped);
         put_out(p.shaped_done, i, (uint8_t)(shaped_done ? 1 : 0));
         if (p.obs && ((r.status & DD_ST_DONE) != 0)) observe(k, s, orow);  // the live path wrote its row
@@ -360,28 +287,9 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
     return ended;
 }
 
-#ifdef DD_EXP_TIMELINE
-// Lab-only (tools/lab/timeline_lab.py): per wave, the 100 MHz real-time clock at
-// kernel entry, loads complete, frame done, obs issued and stores complete,
-// the shader-clock entry/exit, and HW_ID / XCC_ID, for the last launch.
-constexpr int kTlWaves = 1 << 14;
-__device__ uint64_t dd_tl_buf[kTlWaves * 8];
-#define DD_TL(k) tl[k] = __builtin_amdgcn_s_memrealtime()
-#else
-#define DD_TL(k) (void)0
-#endif
-
-// dd_step kernel: one drone per lane, one tile of kStepBlock lanes per block.
-template <typename T, int AFMT, bool kRef, bool kShaped>
-__global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(StepArgs p, Soa<T> a, Soa<T> o) {
-#ifdef DD_EXP_EMPTY  // timing-only: the launch and dispatch floor
-    if (p.n >= 0) return;
-#endif
-#ifdef DD_EXP_TIMELINE
-    uint64_t tl[8];
-    tl[5] = __builtin_amdgcn_s_memtime();
-    DD_TL(0);
-#endif
+// One step tile: one drone per lane, kStepBlock lanes.  `o` is `a` unless kPP.
+template <typename T, int AFMT, bool kRef, int kShape, bool kPP>
+__device__ __forceinline__ void step_tile(const StepArgs& p, const Soa<T>& a, const Soa<T>& o) {
     __shared__ __attribute__((aligned(16))) float tile[kStepBlock * DD_OBS_DIM];
     const uint32_t row0 = blockIdx.x * kStepBlock;
     const uint32_t i = row0 + threadIdx.x;
@@ -390,28 +298,15 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
     // one scalar-load latency later than the state loads could start.
     asm volatile("" ::"s"(a.x), "s"(a.y), "s"(a.vx), "s"(a.vy), "s"(a.angle), "s"(a.omega), "s"(a.fuel),
                  "s"(a.px), "s"(a.py), "s"(a.total), "s"(a.status), "s"(a.steps), "s"(p.actions));
-    if (!p.ping_pong) o = a;  // in place: one set of store bases (SGPRs), as before ping-pong existed
     Raw<T> r;
     if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r);
-#ifdef DD_EXP_PAD_VALU  // timing-only: DD_EXP_PAD_VALU extra f64 FMAs per wave (4 chains), the VALU-cost slope
-    {
-        double pz[4] = {(double)r.x, (double)r.y, (double)r.vx, (double)r.vy};
-#pragma unroll
-        for (int q = 0; q < DD_EXP_PAD_VALU; ++q) asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(pz[q & 3]));
-        asm volatile("" ::"v"(pz[0]), "v"(pz[1]), "v"(pz[2]), "v"(pz[3]));
-    }
-#endif
-#ifdef DD_EXP_TIMELINE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    DD_TL(1);
-#endif
     bool risky = false;
-    bool ended = i < (uint32_t)p.n && finish_lane<T, kRef, kShaped>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM,
-                                                                      &risky);
+    bool ended = i < (uint32_t)p.n &&
+                 finish_lane<T, kRef, kShape, kPP>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM, &risky);
     if (__builtin_expect(__ballot(risky) != 0, 0)) {  // the rare exact pass (frame.h): glibc's sin, cos and pow
-        if (risky) ended = finish_lane<T, kRef, kShaped, true>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM);
+        if (risky)
+            ended = finish_lane<T, kRef, kShape, kPP, true>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM);
     }
-    DD_TL(2);
     if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
         const uint64_t m = __ballot(ended);
         if (m) {
@@ -430,19 +325,20 @@ __global__ __launch_bounds__(kStepBlock, DD_STEP_MIN_WAVES) void step_kernel(Ste
         const int rows = (int)min((int64_t)kWave, max((int64_t)0, (int64_t)p.n - wrow0));
         flush_obs_wave(tile + (threadIdx.x & ~(kWave - 1)) * DD_OBS_DIM, p.obs + (size_t)wrow0 * DD_OBS_DIM, rows);
     }
-#ifdef DD_EXP_TIMELINE
-    DD_TL(3);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    DD_TL(4);
-    tl[6] = __builtin_amdgcn_s_memtime();
-    tl[7] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
-            ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);  // HW_ID, XCC_ID
-    const uint32_t w = (blockIdx.x * kStepBlock + threadIdx.x) / kWave;
-    if ((threadIdx.x & (kWave - 1)) == 0 && w < (uint32_t)kTlWaves) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) dd_tl_buf[w * 8 + k] = tl[k];
-    }
-#endif
+}
+
+// dd_step kernel, in place (the usual case: one set of state bases).
+template <typename T, int AFMT, bool kRef, int kShape>
+__global__ __launch_bounds__(kStepBlock) void step_kernel(StepArgs p, Soa<T> a) {
+    step_tile<T, AFMT, kRef, kShape, false>(p, a, a);
+}
+
+// dd_step kernel with ping-pong state (DDStepIO.state_out): its own
+// instantiation, so the in-place kernel carries none of its plumbing (the
+// shared kernel's `if (!ping_pong) o = a` had cost config 3 ~0.1 us).
+template <typename T, int AFMT, bool kRef, int kShape>
+__global__ __launch_bounds__(kStepBlock) void step_pp_kernel(StepArgs p, Soa<T> a, Soa<T> o) {
+    step_tile<T, AFMT, kRef, kShape, true>(p, a, o);
 }
 
 // ---------------------------------------------------------------------------
@@ -466,12 +362,13 @@ struct RolloutArgs {
     int32_t n;                // lanes in this chunk
     uint64_t action_seed;
     int64_t action_step;
-    // reward_mode="notebook" (kShaped): reward / done above receive the
-    // notebook's calc_reward and done; the engine's go to these (nullable)
-    double* shaped_hist;      // slot 0 of this chunk; slot 1 at + n_total
+    // the notebooks' reward (kShape): reward / done above receive calc_reward
+    // and the notebook's done; the engine's go to these (nullable)
+    double* shaped_hist;      // kShapePpo: slot 0 of this chunk; slot 1 at + n_total
     char* engine_reward;      // frame 0, lane 0 of this chunk (reward_stride apart)
     uint8_t* engine_done;
     int32_t max_steps;
+    int32_t spin_cap;         // kSplit: polls per hand-over wait before it is reported (DD_ERR_HANDOVER)
 };
 
 // DD_ACT_PHILOX: one Philox4x32-10 block (key = action_seed, ctr = {env,
@@ -619,8 +516,10 @@ __device__ __forceinline__ uint32_t buffer_action(__amdgpu_buffer_rsrc_t r, uint
 // the end is normally already satisfied).  Deadlock-free: the writer only
 // waits for frames the frame wave has produced, the frame wave only for the
 // writer to finish frames it has produced.
-// Every wait is bounded (kSpinCap polls of ~64 clocks, ~30 ms): a broken
-// hand-over ends the kernel with wrong rows, never a wave that spins forever.
+// Every wait is bounded (spin_cap polls of ~64 clocks, 2^20 = ~30 ms): a
+// wait that runs out sets DD_ERR_HANDOVER in the device error word
+// (dd_device_errors) and the wave carries on, so a broken hand-over ends the
+// kernel (never a wave that spins forever) and is reported, not silent.
 constexpr int kSpinCap = 1 << 20;
 constexpr int kStageQ = 5;
 
@@ -630,12 +529,29 @@ struct D2 {
 
 // (the value is a VGPR: readfirstlane it where it is tested, so a read issued
 // early does not wait for the LDS at the read)
+// Ordering, under the HIP memory model and not only because LDS executes one
+// wave's operations in issue order: a counter store is preceded by a
+// workgroup-scope release fence over LDS (the slot's data before the counter
+// that publishes it), and a wait that has seen a counter is followed by the
+// matching acquire fence (ctr_acquire).  On gfx950 each is an lgkmcnt(0)
+// wait; the loads themselves stay relaxed so that the frame wave's early read
+// of `consumed` does not wait for the LDS where it is issued.
 __device__ __forceinline__ int ctr_load(const int* c) {
     return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+__device__ __forceinline__ void ctr_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
 __device__ __forceinline__ void ctr_store(int* c, int v) {
-    asm volatile("" ::: "memory");  // after every LDS access before it in program order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The device error word (dd_device_errors): sticky DD_ERR_* bits, one vector
+// atomic from the first active lane of the wave that hits the condition.
+__device__ uint32_t dd_error_bits;
+__device__ __forceinline__ void raise_error(uint32_t bit) {
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)) ==
+        (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1)
+        __hip_atomic_fetch_or(&dd_error_bits, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // slot: this wave's kStageQ x 64 float4 of one frame (float4 q of lane l at q * 64 + l).
@@ -685,16 +601,15 @@ __device__ __forceinline__ void stage_get(const f32x4* slot, uint32_t lane, Lane
     status = q[4][2];
 }
 
-#ifndef DD_ROLL_MIN_WAVES
 // per SIMD: 2 keeps the kernel within 256 registers in all (1 let the Philox-action
 // variant take 2 AGPRs on top of 256 VGPRs, one wave per SIMD at 262,144 drones:
 // +38 %); 4 caps it at 128 VGPRs and spills (A/B: DESIGN.md section 4)
-#define DD_ROLL_MIN_WAVES 2
-#endif
-template <typename T, int AFMT, bool kRef, bool kHeld, bool kShaped, bool kSplit = false>
-__global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) void rollout_kernel(RolloutArgs p,
-                                                                                                  Soa<T> a) {
-    static_assert(!kSplit || (kRef && kHeld && !kShaped), "the split rollout covers the reference config's held path");
+constexpr int kRollMinWaves = 2;
+template <typename T, int AFMT, bool kRef, bool kHeld, int kShape, bool kSplit = false>
+__global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void rollout_kernel(RolloutArgs p,
+                                                                                              Soa<T> a) {
+    static_assert(!kSplit || (kRef && kHeld && kShape == kShapeNone),
+                  "the split rollout covers the reference config's held path");
     // kSplit: the frame hand-over slots (the writer stages its rows in the
     // slot it has just read); otherwise the observation tile
     constexpr int kTileFloats = kSplit ? 4 : kBlock * DD_OBS_DIM + (kHeld ? kHeldPad : 0);
@@ -719,9 +634,15 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             const bool auto_reset = p.k.c.auto_reset;
             double total = at(a.total, hi);  // the running total is the writer's (kDefer)
             for (int f = 0; f < p.frames; ++f) {
-                for (int spin = 0; __builtin_amdgcn_readfirstlane(ctr_load(&ctr[0][wv])) <= f && spin < kSpinCap; ++spin)
+                int spin = 0;
+                for (; __builtin_amdgcn_readfirstlane(ctr_load(&ctr[0][wv])) <= f; ++spin) {
+                    if (spin >= p.spin_cap) {  // the frame wave never produced frame f
+                        raise_error(DD_ERR_HANDOVER);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
-                asm volatile("" ::: "memory");
+                }
+                ctr_acquire();
                 f32x4* slot = &stage[wv][f & 1][0][0];
                 Lane s;
                 uint32_t word;
@@ -747,14 +668,6 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             return;
         }
     }
-#ifdef DD_EXP_S0_LDS
-    constexpr bool kParked = true;
-    __shared__ __attribute__((aligned(16))) LaneRecord<T> parked[kBlock];
-    LaneRecord<T>* const rec = &parked[threadIdx.x];
-#else
-    constexpr bool kParked = false;
-    LaneRecord<T>* const rec = nullptr;
-#endif
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     const uint32_t row0 = blockIdx.x * kBlock;
@@ -773,9 +686,9 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
     constexpr bool kGuard = !kRef && std::is_same<T, double>::value;
     HeldObs held;
     Lane s;
-    // kShaped: the notebook reward's two-frame distance history, in registers
+    // kShapePpo: the notebook reward's two-frame distance history, in registers
     double h0 = 0.0, h1 = 0.0;
-    if constexpr (kShaped) { h0 = at(p.shaped_hist, i); h1 = at(p.shaped_hist + p.n_total, i); }
+    if constexpr (kShape == kShapePpo) { h0 = at(p.shaped_hist, i); h1 = at(p.shaped_hist + p.n_total, i); }
     load_dynamics(a, i, s);
     s.total = at(a.total, i);
     s.status = at(a.status, i);
@@ -830,7 +743,6 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
     asm volatile("" ::"v"(s.x), "v"(s.y), "v"(s.vx), "v"(s.vy), "v"(s.angle), "v"(s.omega), "v"(s.fuel),
                  "v"(s.px), "v"(s.py), "v"(s.total), "v"(s.status), "v"(s.steps), "v"(s.episode), "v"(act0),
                  "v"(act1));
-    if constexpr (kParked) quantize_park<T, false>(s, rec);  // frame 0's starting state (already quantized)
     // auto_reset: the next episode's Philox block per lane (frame.h).  Not with
     // the in-kernel Philox actions, whose own blocks it competes with for
     // registers: there it cost 2-3 % (65,536 and 262,144 x 256), where with
@@ -849,7 +761,6 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             __syncwarp();  // frame f - 1's rows (other lanes of this wave) are in LDS
             hold_obs_wave(tile[(f - 1) & 1] + woff, held);
         }
-        DD_COUNT(6);
         const uint32_t act = kActDw ? __builtin_amdgcn_ubfe(slot, act_sh, 3) : slot;
         if constexpr (AFMT == DD_ACT_PHILOX) {
             slot = rollout_action<AFMT>(p, env, f + 2, i, pa);
@@ -863,8 +774,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
         double reward;
         const bool was_done = (s.status & DD_ST_DONE) != 0;
         auto fast = [&]() __attribute__((always_inline)) {
-            if constexpr (kParked) return frame_checked_parked<kRef, true, T>(k, sw, act, s, rec);
-            else return frame_checked<kRef, true, kSplit>(k, sw, act, s);  // kSplit: the writer finishes it
+            return frame_checked<kRef, true, kSplit>(k, sw, act, s);  // kSplit: the writer finishes it
         };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
@@ -872,7 +782,6 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             // to re-spawn takes the one branch
             reward = fast();
             if (__ballot(was_done)) {
-                DD_COUNT(0);
                 if (was_done) {
                     if constexpr (kAhead) ahead.respawn(sw, k.c.max_fuel, env, s);
                     else spawn(sw, k.c.max_fuel, env, s);
@@ -885,26 +794,32 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
         } else {
             reward = fast();
         }
-        if constexpr (kShaped) {
-            // dd_step's notebook path (finish_lane) with the history in h0 / h1:
-            // slot steps & 1 holds the distance two frames back
+        if constexpr (kShape != kShapeNone) {
+            // dd_step's notebook path (finish_lane); kShapePpo: the history in
+            // h0 / h1, slot steps & 1 holds the distance two frames back
             double v[13];
             observe_values<kGuard, true>(k, s, v);  // the notebook reward's doubles: exact quotients
             double shaped = 0.0;
             bool shaped_done;
             if (kAuto && was_done) {  // re-spawned: the history restarts (prev_state None)
-                h0 = v[9];
-                h1 = __builtin_nan("");
+                if constexpr (kShape == kShapePpo) {
+                    h0 = v[9];
+                    h1 = __builtin_nan("");
+                }
                 shaped_done = false;
             } else if (was_done) {  // sticky done
                 shaped_done = true;
             } else {
-                const bool odd = (s.steps & 1) != 0;
-                shaped = notebook_reward(v, s.status, odd ? h1 : h0);
-                h1 = odd ? v[9] : h1;
-                h0 = odd ? h0 : v[9];
+                if constexpr (kShape == kShapePpo) {
+                    const bool odd = (s.steps & 1) != 0;
+                    shaped = notebook_reward(v, s.status, odd ? h1 : h0);
+                    h1 = odd ? v[9] : h1;
+                    h0 = odd ? h0 : v[9];
+                } else {
+                    shaped = reinforce_reward(v, s.status);
+                }
                 shaped_done = (s.status & DD_ST_DONE) != 0;
-                if (p.max_steps > 0 && s.steps >= p.max_steps) {  // collect_episodes_ppo timeout
+                if (p.max_steps > 0 && s.steps >= p.max_steps) {  // the collection loops' timeout
                     shaped = (s.status & DD_ST_LANDED) ? shaped : shaped - 500;
                     shaped_done = true;
                     s.status |= DD_ST_DONE;
@@ -920,11 +835,15 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
             // hand frame f to the writer (the unrounded frame, as the obs below)
             const int wv = threadIdx.x / kWave;
             // slot f & 1 still holds frame f - 2
-            for (int spin = 0; __builtin_amdgcn_readfirstlane(consumed) < f - 1 && spin < kSpinCap; ++spin) {
+            for (int spin = 0; __builtin_amdgcn_readfirstlane(consumed) < f - 1; ++spin) {
+                if (spin >= p.spin_cap) {  // the writer never finished frame f - 2
+                    raise_error(DD_ERR_HANDOVER);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 consumed = ctr_load(&ctr[1][wv]);
             }
-            asm volatile("" ::: "memory");
+            ctr_acquire();
             stage_put(&stage[wv][f & 1][0][0], threadIdx.x & (kWave - 1), s, s.status | (was_done ? kWasDone : 0u));
             ctr_store(&ctr[0][wv], f + 1);
         } else {
@@ -933,8 +852,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
         }
         if constexpr (kObs && !kSplit) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
         // the obs above sees the unrounded frame, like dd_step's
-        if constexpr (kParked) quantize_park<T, kRef>(s, rec);
-        else quantize<T, kRef>(s);
+        quantize<T, kRef>(s);
         if constexpr (kObs && !kSplit) {
             if constexpr (kHeld) {
                 store_held_wave(held, rsrc_over(obs_prev, prev_bytes));  // frame f - 1's rows
@@ -946,7 +864,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
         }
         rew_p += p.reward_stride;
         done_p += p.n_total;
-        if constexpr (kShaped) {
+        if constexpr (kShape != kShapeNone) {
             erew_p += p.reward_stride;
             edone_p += p.n_total;
         }
@@ -982,7 +900,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, DD_ROLL_MIN_WAVES) vo
     if (live) {
         // every field (lanes may have re-spawned); kSplit: not the total, the writer's
         store_spawn<T, !kSplit>(reload_soa<RolloutArgs, T>(), i, s);
-        if constexpr (kShaped) { at(p.shaped_hist, i) = h0; at(p.shaped_hist + p.n_total, i) = h1; }
+        if constexpr (kShape == kShapePpo) { at(p.shaped_hist, i) = h0; at(p.shaped_hist + p.n_total, i) = h1; }
     }
 }
 
@@ -1214,36 +1132,44 @@ DD_PROBE_KERNEL_(DD_ISA_PROBE)
 // ---------------------------------------------------------------------------
 inline int64_t tiles_of(int64_t n) { return (n + kBlock - 1) / kBlock; }
 
-
-// Lab switches (timing-only builds, tools/build_variants.sh): unused dynamic
-// LDS per block, which caps the blocks a CU takes and so spreads a launch
-// over more CUs.  0 in the product.
-#ifndef DD_EXP_STEP_DYN_LDS
-#define DD_EXP_STEP_DYN_LDS 0
-#endif
-#ifndef DD_EXP_ROLL_DYN_LDS
-#define DD_EXP_ROLL_DYN_LDS 0
-#endif
-
-template <typename T, int AFMT, bool kRef, bool kShaped>
-void launch_step(const StepArgs& p, const Soa<T>& a, const Soa<T>& o, hipStream_t s) {
-    const unsigned blocks = (unsigned)((p.n + kStepBlock - 1) / kStepBlock);
-    hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShaped>), dim3(blocks), dim3(kStepBlock), DD_EXP_STEP_DYN_LDS, s,
-                       p, a, o);
+// The notebook reward a call asks for (frame.h kShape*): REINFORCE's by its
+// mode, PPO's when the history pointer is set, else none.
+inline int shape_of(int32_t shaped_mode, const void* shaped_hist, const void* shaped_reward) {
+    if (shaped_mode == DD_SHAPED_REINFORCE) return kShapeReinforce;
+    return shaped_hist || shaped_reward ? kShapePpo : kShapeNone;
 }
 
-template <typename T, bool kRef, bool kShaped>
-void launch_step_fmt(const StepArgs& p, int afmt, const Soa<T>& a, const Soa<T>& o, hipStream_t s) {
+template <typename T, int AFMT, bool kRef, int kShape>
+void launch_step(const StepArgs& p, const Soa<T>& a, const Soa<T>* o, hipStream_t s) {
+    const unsigned blocks = (unsigned)((p.n + kStepBlock - 1) / kStepBlock);
+    if (o)
+        hipLaunchKernelGGL((step_pp_kernel<T, AFMT, kRef, kShape>), dim3(blocks), dim3(kStepBlock), 0, s, p, a, *o);
+    else
+        hipLaunchKernelGGL((step_kernel<T, AFMT, kRef, kShape>), dim3(blocks), dim3(kStepBlock), 0, s, p, a);
+}
+
+template <typename T, bool kRef, int kShape>
+void launch_step_fmt(const StepArgs& p, int afmt, const Soa<T>& a, const Soa<T>* o, hipStream_t s) {
     switch (afmt) {
-        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK, kRef, kShaped>(p, a, o, s); break;
-        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3, kRef, kShaped>(p, a, o, s); break;
-        default: launch_step<T, DD_ACT_U8X3, kRef, kShaped>(p, a, o, s); break;
+        case DD_ACT_BITMASK: launch_step<T, DD_ACT_BITMASK, kRef, kShape>(p, a, o, s); break;
+        case DD_ACT_F32X3: launch_step<T, DD_ACT_F32X3, kRef, kShape>(p, a, o, s); break;
+        default: launch_step<T, DD_ACT_U8X3, kRef, kShape>(p, a, o, s); break;
+    }
+}
+
+template <typename T, bool kRef>
+void launch_step_shape(const StepArgs& p, int shape, int afmt, const Soa<T>& a, const Soa<T>* o, hipStream_t s) {
+    switch (shape) {
+        case kShapeNone: launch_step_fmt<T, kRef, kShapeNone>(p, afmt, a, o, s); break;
+        case kShapePpo: launch_step_fmt<T, kRef, kShapePpo>(p, afmt, a, o, s); break;
+        default: launch_step_fmt<T, kRef, kShapeReinforce>(p, afmt, a, o, s); break;
     }
 }
 
 template <typename T>
 void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, hipStream_t s) {
     const bool ref = uses_reference_physics(p.k.c);
+    const int shape = shape_of(io.shaped_mode, io.shaped_hist, io.shaped_reward);
     const int64_t act_w = io.action_format == DD_ACT_F32X3 ? 12 : io.action_format == DD_ACT_U8X3 ? 3 : 1;
     for (int64_t first = 0; first < n; first += kChunk) {
         const int64_t len = n - first < kChunk ? n - first : kChunk;
@@ -1253,22 +1179,16 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
         p.obs = io.obs ? io.obs + first * DD_OBS_DIM : nullptr;
         p.n = (int32_t)len;
         p.idx_base = (int32_t)first;
-        const bool shaped = io.shaped_hist != nullptr;
-        p.shaped_hist = shaped ? io.shaped_hist + first : nullptr;
+        p.shaped_hist = shape == kShapePpo ? io.shaped_hist + first : nullptr;
         p.hist_stride = n;
-        p.shaped_reward = shaped ? static_cast<void*>(static_cast<T*>(io.shaped_reward) + first) : nullptr;
-        p.shaped_done = shaped ? io.shaped_done + first : nullptr;
+        p.shaped_reward = shape != kShapeNone ? static_cast<void*>(static_cast<T*>(io.shaped_reward) + first) : nullptr;
+        p.shaped_done = shape != kShapeNone ? io.shaped_done + first : nullptr;
         p.max_steps = io.max_steps;
         const Soa<T> a = soa_of<T>(st, first);
-        const Soa<T> o = io.state_out ? soa_of<T>(*io.state_out, first) : a;
-        p.ping_pong = io.state_out ? 1 : 0;
-        if (ref) {
-            if (shaped) launch_step_fmt<T, true, true>(p, io.action_format, a, o, s);
-            else launch_step_fmt<T, true, false>(p, io.action_format, a, o, s);
-        } else {
-            if (shaped) launch_step_fmt<T, false, true>(p, io.action_format, a, o, s);
-            else launch_step_fmt<T, false, false>(p, io.action_format, a, o, s);
-        }
+        Soa<T> o;
+        if (io.state_out) o = soa_of<T>(*io.state_out, first);
+        if (ref) launch_step_shape<T, true>(p, shape, io.action_format, a, io.state_out ? &o : nullptr, s);
+        else launch_step_shape<T, false>(p, shape, io.action_format, a, io.state_out ? &o : nullptr, s);
     }
 }
 
@@ -1276,13 +1196,7 @@ void step_chunks(StepArgs p, const DDState& st, const DDStepIO& io, int64_t n, h
 // CU or fewer: its block takes 8 waves of ~256 registers, all of a CU's
 // register file for 256 drones, where the single-role kernel fits two blocks
 // (262,144 drones: 4 rounds of split blocks against 2 of single-role ones).
-// DD_ROLL_SPLIT=0 in the environment (read once) keeps the single-role kernel.
 inline bool split_rollout_fits(unsigned blocks) {
-    static const bool enabled = [] {
-        const char* e = getenv("DD_ROLL_SPLIT");
-        return !(e && e[0] == '0');
-    }();
-    if (!enabled) return false;
     static int cus[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
@@ -1291,46 +1205,65 @@ inline bool split_rollout_fits(unsigned blocks) {
     return blocks <= (unsigned)cus[dev];
 }
 
-template <typename T, int AFMT, bool kRef, bool kShaped>
-void launch_rollout(const RolloutArgs& p, const Soa<T>& a, hipStream_t s) {
-    // the held obs path needs every frame row start 16-byte aligned, and
-    // (bitmask actions) a 4-byte aligned action buffer for its dword loads
-    const bool held = (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 && (p.n_total & 3) == 0 &&
-                      (AFMT != DD_ACT_BITMASK || (reinterpret_cast<uintptr_t>(p.actions) & 3u) == 0);
+// Which rollout kernel a launch of n lanes takes (DD_ROLLOUT_*): the held
+// observation path needs every frame row start 16-byte aligned and (bitmask
+// actions) a 4-byte aligned action buffer for its dword loads; the split
+// kernel covers the reference world's held path with the engine reward.
+inline int rollout_kernel_for(bool ref, int shape, int afmt, const void* actions, const float* obs, int64_t n_total,
+                              int64_t n, int32_t choice) {
+    const bool held = (reinterpret_cast<uintptr_t>(obs) & 15u) == 0 && (n_total & 3) == 0 &&
+                      (afmt != DD_ACT_BITMASK || (reinterpret_cast<uintptr_t>(actions) & 3u) == 0);
+    if (ref && shape == kShapeNone && held && obs && choice != DD_ROLLOUT_SINGLE &&
+        split_rollout_fits((unsigned)tiles_of(n)))
+        return DD_ROLLOUT_SPLIT;
+    return held ? DD_ROLLOUT_HELD : DD_ROLLOUT_FLUSHED;
+}
+
+template <typename T, int AFMT, bool kRef, int kShape>
+void launch_rollout(const RolloutArgs& p, int kind, const Soa<T>& a, hipStream_t s) {
     const unsigned blocks = (unsigned)tiles_of(p.n);
-    if constexpr (kRef && !kShaped) {
-        if (held && p.obs && split_rollout_fits(blocks)) {
-            hipLaunchKernelGGL((rollout_kernel<T, AFMT, true, true, false, true>), dim3(blocks), dim3(2 * kBlock),
-                               DD_EXP_ROLL_DYN_LDS, s, p, a);
+    if constexpr (kRef && kShape == kShapeNone) {
+        if (kind == DD_ROLLOUT_SPLIT) {
+            hipLaunchKernelGGL((rollout_kernel<T, AFMT, true, true, kShapeNone, true>), dim3(blocks), dim3(2 * kBlock),
+                               0, s, p, a);
             return;
         }
     }
-    if (held)
-        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true, kShaped>), dim3(blocks), dim3(kBlock),
-                           DD_EXP_ROLL_DYN_LDS, s, p, a);
+    if (kind != DD_ROLLOUT_FLUSHED)
+        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, true, kShape>), dim3(blocks), dim3(kBlock), 0, s, p, a);
     else
-        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false, kShaped>), dim3(blocks), dim3(kBlock),
-                           DD_EXP_ROLL_DYN_LDS, s, p, a);
+        hipLaunchKernelGGL((rollout_kernel<T, AFMT, kRef, false, kShape>), dim3(blocks), dim3(kBlock), 0, s, p, a);
 }
 
-template <typename T, bool kRef, bool kShaped>
-void launch_rollout_fmt(const RolloutArgs& p, int afmt, const Soa<T>& a, hipStream_t s) {
+template <typename T, bool kRef, int kShape>
+void launch_rollout_fmt(const RolloutArgs& p, int kind, int afmt, const Soa<T>& a, hipStream_t s) {
     switch (afmt) {
-        case DD_ACT_BITMASK: launch_rollout<T, DD_ACT_BITMASK, kRef, kShaped>(p, a, s); break;
-        case DD_ACT_F32X3: launch_rollout<T, DD_ACT_F32X3, kRef, kShaped>(p, a, s); break;
-        case DD_ACT_U8X3: launch_rollout<T, DD_ACT_U8X3, kRef, kShaped>(p, a, s); break;
-        default: launch_rollout<T, DD_ACT_PHILOX, kRef, kShaped>(p, a, s); break;
+        case DD_ACT_BITMASK: launch_rollout<T, DD_ACT_BITMASK, kRef, kShape>(p, kind, a, s); break;
+        case DD_ACT_F32X3: launch_rollout<T, DD_ACT_F32X3, kRef, kShape>(p, kind, a, s); break;
+        case DD_ACT_U8X3: launch_rollout<T, DD_ACT_U8X3, kRef, kShape>(p, kind, a, s); break;
+        default: launch_rollout<T, DD_ACT_PHILOX, kRef, kShape>(p, kind, a, s); break;
+    }
+}
+
+template <typename T, bool kRef>
+void launch_rollout_shape(const RolloutArgs& p, int kind, int shape, int afmt, const Soa<T>& a, hipStream_t s) {
+    switch (shape) {
+        case kShapeNone: launch_rollout_fmt<T, kRef, kShapeNone>(p, kind, afmt, a, s); break;
+        case kShapePpo: launch_rollout_fmt<T, kRef, kShapePpo>(p, kind, afmt, a, s); break;
+        default: launch_rollout_fmt<T, kRef, kShapeReinforce>(p, kind, afmt, a, s); break;
     }
 }
 
 template <typename T>
 void rollout_chunks(RolloutArgs p, const DDState& st, const DDRolloutIO& io, int64_t n, hipStream_t s) {
     const bool ref = uses_reference_physics(p.k.c);
+    const int shape = shape_of(io.shaped_mode, io.shaped_hist, nullptr);
     const int64_t act_w = io.action_format == DD_ACT_F32X3 ? 12 : io.action_format == DD_ACT_U8X3 ? 3
                         : io.action_format == DD_ACT_BITMASK ? 1 : 0;
     p.act_stride = n * act_w;
     p.reward_stride = n * (int64_t)sizeof(T);
     p.n_total = n;
+    p.spin_cap = io.kernel == DD_ROLLOUT_SPLIT_NO_WAIT ? 0 : kSpinCap;
     const int32_t frames = p.frames;
     const int64_t step0 = p.action_step;
     for (int64_t first = 0; first < n; first += kChunk) {
@@ -1355,20 +1288,15 @@ void rollout_chunks(RolloutArgs p, const DDState& st, const DDRolloutIO& io, int
             p.done = io.done + g0 * n + first;
             p.obs = io.obs ? io.obs + (g0 * n + first) * DD_OBS_DIM : nullptr;
             p.n = (int32_t)len;
-            const bool shaped = io.shaped_hist != nullptr;
-            p.shaped_hist = shaped ? io.shaped_hist + first : nullptr;
-            p.engine_reward = shaped && io.engine_reward
+            p.shaped_hist = shape == kShapePpo ? io.shaped_hist + first : nullptr;
+            p.engine_reward = shape != kShapeNone && io.engine_reward
                                   ? reinterpret_cast<char*>(static_cast<T*>(io.engine_reward) + g0 * n + first) : nullptr;
-            p.engine_done = shaped && io.engine_reward ? io.engine_done + g0 * n + first : nullptr;
+            p.engine_done = shape != kShapeNone && io.engine_reward ? io.engine_done + g0 * n + first : nullptr;
             p.max_steps = io.max_steps;
             const Soa<T> a = soa_of<T>(st, first);
-            if (ref) {
-                if (shaped) launch_rollout_fmt<T, true, true>(p, io.action_format, a, s);
-                else launch_rollout_fmt<T, true, false>(p, io.action_format, a, s);
-            } else {
-                if (shaped) launch_rollout_fmt<T, false, true>(p, io.action_format, a, s);
-                else launch_rollout_fmt<T, false, false>(p, io.action_format, a, s);
-            }
+            const int kind = rollout_kernel_for(ref, shape, io.action_format, p.actions, p.obs, n, len, io.kernel);
+            if (ref) launch_rollout_shape<T, true>(p, kind, shape, io.action_format, a, s);
+            else launch_rollout_shape<T, false>(p, kind, shape, io.action_format, a, s);
         }
     }
 }
@@ -1379,17 +1307,6 @@ int finish() { return (int)hipGetLastError(); }
 
 extern "C" {
 
-#ifdef DD_EXP_COUNT
-int dd_lab_counts(unsigned long long* out, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dd::dd_lab_counts), sizeof(unsigned long long) * 8);
-    if (e == hipSuccess && reset) {
-        static const unsigned long long z[8] = {};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(dd::dd_lab_counts), z, sizeof(z));
-    }
-    return e;
-}
-#endif
-
 void dd_config_default(DDConfig* c) {
     if (c) *c = dd::reference_config();
 }
@@ -1399,8 +1316,14 @@ int dd_step(const DDConfig* cfg, const DDState* st, const DDStepIO* io, int64_t 
     if (io->action_format < DD_ACT_BITMASK || io->action_format > DD_ACT_U8X3) return hipErrorInvalidValue;
     if (st->precision != DD_F32 && st->precision != DD_F64) return hipErrorInvalidValue;
     if (io->done_idx && !io->done_count) return hipErrorInvalidValue;
-    const int shaped_ptrs = (io->shaped_hist != nullptr) + (io->shaped_reward != nullptr) + (io->shaped_done != nullptr);
-    if (shaped_ptrs != 0 && shaped_ptrs != 3) return hipErrorInvalidValue;
+    if (io->shaped_mode == DD_SHAPED_REINFORCE) {  // no history: shaped_hist is not read
+        if (!io->shaped_reward || !io->shaped_done) return hipErrorInvalidValue;
+    } else if (io->shaped_mode == DD_SHAPED_PPO) {
+        const int ptrs = (io->shaped_hist != nullptr) + (io->shaped_reward != nullptr) + (io->shaped_done != nullptr);
+        if (ptrs != 0 && ptrs != 3) return hipErrorInvalidValue;
+    } else {
+        return hipErrorInvalidValue;
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (io->done_count) {
         const hipError_t e = hipMemsetAsync(io->done_count, 0, sizeof(int32_t), s);
@@ -1436,7 +1359,10 @@ int dd_rollout(const DDConfig* cfg, const DDState* st, const DDRolloutIO* io, in
     if (!dd::state_ok(st) || !io->reward || !io->done) return hipErrorInvalidValue;
     if (io->action_format != DD_ACT_PHILOX && !io->actions) return hipErrorInvalidValue;
     if ((io->engine_reward != nullptr) != (io->engine_done != nullptr)) return hipErrorInvalidValue;
-    if (io->engine_reward && !io->shaped_hist) return hipErrorInvalidValue;
+    if (io->shaped_mode != DD_SHAPED_PPO && io->shaped_mode != DD_SHAPED_REINFORCE) return hipErrorInvalidValue;
+    if (io->engine_reward && dd::shape_of(io->shaped_mode, io->shaped_hist, nullptr) == dd::kShapeNone)
+        return hipErrorInvalidValue;
+    if (io->kernel < DD_ROLLOUT_AUTO || io->kernel > DD_ROLLOUT_SPLIT_NO_WAIT) return hipErrorInvalidValue;
     hipStream_t s = static_cast<hipStream_t>(stream);
     dd::RolloutArgs p{};
     p.k = dd::make_consts(*cfg);
@@ -1446,6 +1372,23 @@ int dd_rollout(const DDConfig* cfg, const DDState* st, const DDRolloutIO* io, in
     if (st->precision == DD_F32) dd::rollout_chunks<float>(p, *st, *io, n, s);
     else dd::rollout_chunks<double>(p, *st, *io, n, s);
     return dd::finish();
+}
+
+int dd_rollout_kernel(const DDConfig* cfg, const DDState* st, const DDRolloutIO* io, int64_t n) {
+    if (!cfg || !io || !st || n <= 0 || n > INT32_MAX) return -1;
+    const int64_t len = n < dd::kChunk ? n : dd::kChunk;
+    return dd::rollout_kernel_for(dd::uses_reference_physics(*cfg), dd::shape_of(io->shaped_mode, io->shaped_hist, nullptr),
+                                  io->action_format, io->actions, io->obs, n, len, io->kernel);
+}
+
+int dd_device_errors(uint32_t* bits, int32_t clear) {
+    if (!bits) return hipErrorInvalidValue;
+    hipError_t e = hipMemcpyFromSymbol(bits, HIP_SYMBOL(dd::dd_error_bits), sizeof(uint32_t), 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && clear) {
+        static const uint32_t zero = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(dd::dd_error_bits), &zero, sizeof(uint32_t), 0, hipMemcpyHostToDevice);
+    }
+    return (int)e;
 }
 
 int dd_reset(const DDConfig* cfg, const DDState* st, const uint8_t* mask, float* obs, int64_t n, void* stream) {
@@ -1583,15 +1526,6 @@ int64_t dd_step_bytes_per_env(int32_t precision, int32_t action_format, int32_t 
 const char* dd_error_string(int code) { return hipGetErrorString((hipError_t)code); }
 
 int dd_abi_version(void) { return DD_ABI_VERSION; }
-
-#ifdef DD_EXP_TIMELINE
-// Lab-only: copies the last step launch's per-wave timeline (8 x u64 per wave).
-int dd_lab_timeline(void* dst, int64_t bytes) {
-    const int64_t cap = (int64_t)sizeof(uint64_t) * 8 * dd::kTlWaves;
-    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(dd::dd_tl_buf), (size_t)(bytes < cap ? bytes : cap), 0,
-                                    hipMemcpyDeviceToHost);
-}
-#endif
 
 }  // extern "C"
 #endif  // DD_ISA_PROBE

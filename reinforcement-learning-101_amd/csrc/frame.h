@@ -26,12 +26,7 @@ __device__ const uint64_t dd_libm_exp_tab[256] = DD_LIBM_EXP_TAB;
 __device__ const double dd_libm_sincos_tab[440] = DD_LIBM_SINCOS_TAB;
 #define DD_LIBM_FN __device__ __forceinline__
 #define DD_LIBM_OPAQUE
-#ifdef DD_EXP_LIBM_CALLS
-#define DD_LIBM_ENTRY __device__ __noinline__
-#define DD_LIBM_SINCOS_FN __device__ __noinline__
-#else
 #define DD_LIBM_ENTRY __device__ __forceinline__
-#endif
 #include "libm_ref.h"
 #undef DD_LIBM_FN
 #undef DD_LIBM_ENTRY
@@ -45,11 +40,9 @@ constexpr double kDeg2Rad = 3.14159265358979323846 / 180.0;
 
 // sin and cos of an angle in degrees, as rotate_point computes them
 // (physics.py:16-18: np.radians, then np.cos and np.sin).  Fast: trig.h's
-// (within an ulp of glibc's); kExact: glibc's, bit for bit (libm_ref.h), for
-// the rare frames where an ulp could flip a flag (frame).  Lab switches for
-// the fast one: DD_TRIG_GLIBC (glibc's everywhere: +9 % step, +26 % rollout
-// with the table in global memory), DD_TRIG_OCML (the ROCm device
-// library's), DD_EXP_FAKE_TRIG (timing only).
+// (within an ulp of glibc's; glibc's everywhere measured +9 % step, +26 %
+// rollout; OCML's sincos equal within noise); kExact: glibc's, bit for bit
+// (libm_ref.h), for the rare frames where an ulp could flip a flag (frame).
 // kSgpr: the polynomial coefficients as SGPR operands (trig::hstep_c), for
 // the step kernel, whose four waves per SIMD overlap one wave's scalar moves
 // with another's VALU; the loops (one wave per SIMD) keep the vector form.
@@ -59,18 +52,7 @@ __device__ __forceinline__ void sincos_deg(double deg, double* s, double* c) {
         libm::sincos(deg * kDeg2Rad, s, c);
         return;
     }
-#if defined(DD_EXP_FAKE_TRIG)  // timing-only sensitivity: what the trig costs
-    *s = deg * 1e-3;
-    *c = 1.0 - fabs(*s);
-#elif defined(DD_TRIG_OCML)
-    ::sincos(deg * kDeg2Rad, s, c);
-#elif defined(DD_TRIG_GLIBC)
-    libm::sincos(deg * kDeg2Rad, s, c);
-#elif defined(DD_EXP_TRIG_VCOEF)
-    trig::sincos<false>(deg * kDeg2Rad, s, c);
-#else
     trig::sincos<kSgpr>(deg * kDeg2Rad, s, c);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -203,24 +185,16 @@ struct Lane {
 // (lab medians, with the SGPR coefficients and the kRef thrust).  The loops
 // keep sqrt(): their frame is one basic block, and the branch splitting it
 // cost more than the four VALU it saves per root (65,536 x 256 rollout
-// 0.362 -> 0.371 ms, profiles/r03/lab/valu_trims_ab.jsonl).  DD_SQRT_LLVM:
-// sqrt() everywhere, for A/B runs.
+// 0.362 -> 0.371 ms, profiles/r03/lab/valu_trims_ab.jsonl).
 template <bool kUnscaled = false>
 __device__ __forceinline__ double measure(Lane& s) {
     const double dx = s.px - s.x, dy = s.py - s.y;
     const double ss = s.vx * s.vx + s.vy * s.vy;
     const double dd = dx * dx + dy * dy;
-#ifdef DD_EXP_FAKE_SQRT  // timing-only sensitivity: what the two square roots cost
-    s.speed = ss * 0.25;
-    s.dist = dd * 0.001;
-#else
-#ifndef DD_SQRT_LLVM
     if (!kUnscaled) {
-#endif
         s.speed = sqrt(ss);
         s.dist = sqrt(dd);
         return ss;
-#ifndef DD_SQRT_LLVM
     }
     if (__builtin_expect(__ballot(!(ss >= 0x1p-767) | !(dd >= 0x1p-767)) != 0, 0)) {
         s.speed = sqrt(ss);
@@ -229,25 +203,8 @@ __device__ __forceinline__ double measure(Lane& s) {
         s.speed = trig::sqrt_unscaled(ss);
         s.dist = trig::sqrt_unscaled(dd);
     }
-#endif
-#endif
     return ss;
 }
-
-// Lab-only (-DDD_EXP_COUNT, tools/lab/branch_count_lab.py): how many
-// wave-frames enter each rare branch (one count per wave that enters it).
-#ifdef DD_EXP_COUNT
-static __device__ unsigned long long dd_lab_counts[8];
-#define DD_COUNT(i)                                                                       \
-    do {                                                                                  \
-        const uint64_t m_ = __ballot(1);                                                  \
-        if ((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(m_)) atomicAdd(&dd_lab_counts[i], 1ull); \
-    } while (0)
-#else
-#define DD_COUNT(i) \
-    do {            \
-    } while (0)
-#endif
 
 // DroneGame.reset (game_engine.py:59-93) + Drone.reset (drone.py:221-238) +
 // Platform.reset (platform.py:104-114).  `c` is the call's config (switches,
@@ -257,15 +214,8 @@ static __device__ unsigned long long dd_lab_counts[8];
 // `episode += 1`.
 // The Philox block of (seed; env, episode) that a re-spawn draws from.
 __device__ __forceinline__ void spawn_words(const DDConfig& c, int64_t env, int32_t episode, uint32_t (&r)[4]) {
-#ifdef DD_EXP_FAKE_SPAWN  // timing-only sensitivity: what the re-spawn's Philox block costs
-    r[0] = (uint32_t)env * 0x9E3779B9u ^ (uint32_t)episode;
-    r[1] = r[0] * 0x85EBCA6Bu;
-    r[2] = r[1] * 0xC2B2AE35u;
-    r[3] = r[2] * 0x27D4EB2Fu;
-#else
     philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)episode, 0u, (uint32_t)c.seed,
                   (uint32_t)(c.seed >> 32), r);
-#endif
 }
 
 // The re-spawn of a lane whose episode counter is already the new episode's,
@@ -295,11 +245,7 @@ __device__ __forceinline__ void spawn_from(const DDConfig& c, double max_fuel, c
     // least 1, inside trig::sqrt_unscaled's exact range
     const double dx = s.px - s.x, dy = s.py - s.y;
     s.speed = 0.0;
-#if defined(DD_SQRT_LLVM) || defined(DD_EXP_FAKE_SQRT)
-    s.dist = sqrt(dx * dx + dy * dy);
-#else
     s.dist = trig::sqrt_unscaled(dx * dx + dy * dy);
-#endif
 }
 
 __device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_t env, Lane& s) {
@@ -321,10 +267,9 @@ __device__ __forceinline__ void spawn(const DDConfig& c, double max_fuel, int64_
 struct SpawnAhead {
     uint32_t r[4];
     int32_t ep;  // the episode r was drawn for
-#ifndef DD_SPAWN_REFILL
-#define DD_SPAWN_REFILL 32  // frames between refills (a power of two; lab knob)
-#endif
-    static constexpr int kRefill = DD_SPAWN_REFILL;
+    // frames between refills (a power of two): 4 / 8 / 16 / 32 frames measured
+    // 0.303 / 0.295 / 0.293 / 0.288 ms (config 5; 64 no better), DESIGN.md §4
+    static constexpr int kRefill = 32;
 
     __device__ __forceinline__ void init(const DDConfig& c, int64_t env, int32_t episode) {
         ep = episode + 1;
@@ -357,7 +302,6 @@ __device__ __forceinline__ double wrap_angle(double a) {
     double w = a > 180.0 ? a - 360.0 : a;
     w = a < -180.0 ? a + 360.0 : w;
     if (__builtin_expect(fabs(a) > 540.0, 0)) {
-        DD_COUNT(4);
         w = trig::normalize_angle(a);
     }
     return w;
@@ -419,22 +363,6 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         thrust(sa, ca, &dvx, &dvy);
         s.vx = main_on ? s.vx + dvx : s.vx;
         s.vy = main_on ? s.vy + dvy : s.vy;
-#ifdef DD_EXP_SEL
-      if constexpr (kRef) {
-        // (config.py's finite constants) the gated fuel and spin terms as a
-        // selected operand instead of a selected result: x - 0.0 and
-        // x + (-0.0) are x for every x (signed zeros included), and a
-        // selected term gives the reference's one rounding (fma with a factor
-        // of 1.0 is the plain sum); each select is one v_cndmask on a high
-        // word (the low words are zero)
-        s.fuel = s.fuel - (main_on ? c.fuel_main : 0.0);
-        const bool left_on = (act & 2u) && s.fuel > 0.0;
-        s.omega = fma(-c.side_thrust_power, left_on ? 1.0 : 0.0, s.omega);
-        s.fuel = s.fuel - (left_on ? c.fuel_side : 0.0);
-        const bool right_on = (act & 4u) && s.fuel > 0.0;
-        s.omega = fma(c.side_thrust_power, right_on ? 1.0 : -0.0, s.omega);
-        s.fuel = s.fuel - (right_on ? c.fuel_side : 0.0);
-      } else {
         s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
         const bool left_on = (act & 2u) && s.fuel > 0.0;
         s.omega = left_on ? s.omega - c.side_thrust_power : s.omega;
@@ -442,16 +370,6 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         const bool right_on = (act & 4u) && s.fuel > 0.0;
         s.omega = right_on ? s.omega + c.side_thrust_power : s.omega;
         s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
-      }
-#else
-        s.fuel = main_on ? s.fuel - c.fuel_main : s.fuel;
-        const bool left_on = (act & 2u) && s.fuel > 0.0;
-        s.omega = left_on ? s.omega - c.side_thrust_power : s.omega;
-        s.fuel = left_on ? s.fuel - c.fuel_side : s.fuel;
-        const bool right_on = (act & 4u) && s.fuel > 0.0;
-        s.omega = right_on ? s.omega + c.side_thrust_power : s.omega;
-        s.fuel = right_on ? s.fuel - c.fuel_side : s.fuel;
-#endif
     } else {
         if (main_on) {
             double sa, ca, dvx, dvy;
@@ -475,11 +393,7 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     s.y += s.vy * c.dt;
     s.angle += s.omega * c.dt;
     s.omega *= c.angular_drag;
-#ifdef DD_EXP_STEP_WRAP_SELECT
-    s.angle = wrap_angle(s.angle);
-#else
-    s.angle = kFlat ? wrap_angle(s.angle) : trig::normalize_angle(s.angle);
-#endif
+    s.angle = kFlat ? wrap_angle(s.angle) : trig::normalize_angle(s.angle);  // (the select form: step +-1 %)
 
     if (!kRef && sw.platform_moving) {
         const double dir = (s.status & DD_ST_PLAT_LEFT) ? -1.0 : 1.0;
@@ -536,17 +450,8 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     const double rx = c.platform_half_width + fabs(c.drone_half_height);
     const double ry = c.platform_half_height + fabs(c.drone_half_height);
     const double slack = 1.0 + 1e-9 * (fabs(s.x) + fabs(s.y) + fabs(s.px) + fabs(s.py) + rx + ry);
-#ifdef DD_EXP_FLAT_NEAR
-    // kFlat: the three tests as one predicate (bitwise &: no short-circuit),
-    // so the rare body sits behind one exec-mask branch instead of three
-    // nested ones that most waves enter (upright lanes are common)
-    const bool near_pad = kFlat ? (upright & (fabs(s.x - s.px) <= rx + slack) & (fabs(s.y - s.py) <= ry + slack))
-                                : (upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack);
-#else
     const bool near_pad = upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack;
-#endif
     if (near_pad) {
-        DD_COUNT(2);
         // (lanes out of this reach of the pad: on_pad = false exactly as the
         // reference's comparisons give, the bottom centre lying within
         // |half_height| (+ rounding) of (x, y); NaN fails both tests alike)
@@ -567,7 +472,6 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
             risky |= edge;
         }
         if (slow) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
-            DD_COUNT(3);
             double sb, cb;
             sincos_deg<kExact, kSgpr>(s.angle, &sb, &cb);
             const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
@@ -655,161 +559,17 @@ __device__ __forceinline__ double finish_deferred(Lane& s, bool was_done, bool a
 
 // A frame for kernels that keep the lane's state in registers (the rollout
 // loops): the fast frame, and for a lane it reports risky the frame again
-// from the kept state with glibc's functions (a wave-uniform rare branch).
-#ifdef DD_EXP_EXACT_CALL
-struct ExactFrame {
-    Lane s;
-    double reward;
-};
-// by value: a Lane& would make the caller's state address-taken (scratch)
-template <bool kRef>
-__device__ __noinline__ ExactFrame frame_exact_call(const Consts* kp, const DDConfig* swp, uint32_t act, Lane s) {
-    const Consts& k = kRef ? kRefConsts : *kp;
-    ExactFrame r;
-    r.reward = frame<kRef, false, true>(k, kRef ? kRefConsts.c : *swp, act, s, nullptr);
-    r.s = s;
-    return r;
-}
-#endif
-
-#ifdef DD_EXP_EXACT_LDS
-struct ExactSlot {
-    double x, y, vx, vy, angle, omega, fuel, px, py, total, reward;
-    uint32_t status;
-    int32_t steps, episode;
-};
-typedef __attribute__((address_space(3))) ExactSlot* ExactSlotPtr;
-template <bool kRef>
-__device__ __noinline__ void frame_exact_lds(const Consts* kp, const DDConfig* swp, uint32_t act, ExactSlotPtr q) {
-    const Consts& k = kRef ? kRefConsts : *kp;
-    Lane s;
-    s.x = q->x; s.y = q->y; s.vx = q->vx; s.vy = q->vy; s.angle = q->angle; s.omega = q->omega;
-    s.fuel = q->fuel; s.px = q->px; s.py = q->py; s.total = q->total;
-    s.status = q->status; s.steps = q->steps; s.episode = q->episode;
-    s.speed = 0.0; s.dist = 0.0;
-    q->reward = frame<kRef, false, true>(k, kRef ? kRefConsts.c : *swp, act, s, nullptr);
-    q->x = s.x; q->y = s.y; q->vx = s.vx; q->vy = s.vy; q->angle = s.angle; q->omega = s.omega;
-    q->fuel = s.fuel; q->px = s.px; q->py = s.py; q->total = s.total;
-    q->status = s.status; q->steps = s.steps;
-}
-#endif
-
+// from the kept state with glibc's functions (a wave-uniform rare branch; as
+// an out-of-line call, or through an LDS slot, it measured slower or equal,
+// DESIGN.md §3.2).
 template <bool kRef, bool kFlat, bool kDefer = false>
 __device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
     const Lane s0 = s;
     bool risky = false;
     double reward = frame<kRef, kFlat, false, kDefer>(k, sw, act, s, &risky);
-#ifdef DD_EXP_RISKY_ONLY
-    if (__builtin_expect(__ballot(risky) != 0, 0)) {
-        if (risky) reward = __builtin_nan("");
-    }
-#elif defined(DD_EXP_EXACT_LDS)
     if (__builtin_expect(__ballot(risky) != 0, 0)) {
         if (risky) {
-            __shared__ ExactSlot slots[256];
-            ExactSlotPtr q = (ExactSlotPtr)&slots[threadIdx.x & 255];
-            q->x = s0.x; q->y = s0.y; q->vx = s0.vx; q->vy = s0.vy; q->angle = s0.angle; q->omega = s0.omega;
-            q->fuel = s0.fuel; q->px = s0.px; q->py = s0.py; q->total = s0.total;
-            q->status = s0.status; q->steps = s0.steps; q->episode = s0.episode;
-            frame_exact_lds<kRef>(kRef ? nullptr : &k, kRef ? nullptr : &sw, act, q);
-            s.x = q->x; s.y = q->y; s.vx = q->vx; s.vy = q->vy; s.angle = q->angle; s.omega = q->omega;
-            s.fuel = q->fuel; s.px = q->px; s.py = q->py; s.total = q->total;
-            s.status = q->status; s.steps = q->steps;
-            measure(s);
-            reward = q->reward;
-        }
-    }
-#elif !defined(DD_EXP_NO_EXACT)
-    if (__builtin_expect(__ballot(risky) != 0, 0)) {
-        DD_COUNT(1);
-        if (risky) {
-#ifdef DD_EXP_EXACT_CALL
-            const ExactFrame e = frame_exact_call<kRef>(kRef ? nullptr : &k, kRef ? nullptr : &sw, act, s0);
-            s = e.s;
-            reward = e.reward;
-#else
             s = s0;
-            reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
-#endif
-        }
-    }
-#endif
-    return reward;
-}
-
-// The state a frame starts from, parked in LDS (one record per lane) for the
-// rare exact redo of a rollout loop, instead of a register copy of the Lane
-// that stays live across the whole fast frame (frame_checked's s0: 27 VGPRs
-// at the kernel's register limit).  Written by quantize_park at the end of
-// every frame (the storage-width values quantize makes anyway, so no extra
-// conversion) and once before the first; read back only by a risky lane.
-// Storage width T: float records are 16 dwords, double records 24, both as
-// 16-byte LDS writes.
-template <typename T>
-struct LaneRecord {
-    uint32_t w[sizeof(T) == 4 ? 16 : 24];
-};
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
-template <typename T>
-__device__ __forceinline__ void park_lane(LaneRecord<T>* rec, const T v[10], uint32_t status, int32_t steps,
-                                          int32_t episode) {
-    uint32_t w[sizeof(T) == 4 ? 16 : 24];
-    memcpy(w, v, 10 * sizeof(T));
-    constexpr int o = 10 * sizeof(T) / 4;
-    w[o] = status;
-    w[o + 1] = (uint32_t)steps;
-    w[o + 2] = (uint32_t)episode;
-#pragma unroll
-    for (int q = o + 3; q < (int)(sizeof(w) / 4); ++q) w[q] = 0u;
-    u32x4_t* d = reinterpret_cast<u32x4_t*>(rec->w);
-#pragma unroll
-    for (int q = 0; q < (int)(sizeof(w) / 16); ++q) d[q] = u32x4_t{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
-}
-
-template <typename T>
-__device__ __forceinline__ void unpark_lane(const LaneRecord<T>* rec, Lane& s) {
-    uint32_t w[sizeof(T) == 4 ? 16 : 24];
-    const u32x4_t* d = reinterpret_cast<const u32x4_t*>(rec->w);
-#pragma unroll
-    for (int q = 0; q < (int)(sizeof(w) / 16); ++q) {
-        const u32x4_t x = d[q];
-        w[4 * q] = x[0]; w[4 * q + 1] = x[1]; w[4 * q + 2] = x[2]; w[4 * q + 3] = x[3];
-    }
-    T v[10];
-    memcpy(v, w, 10 * sizeof(T));
-    constexpr int o = 10 * sizeof(T) / 4;
-    s.x = v[0]; s.y = v[1]; s.vx = v[2]; s.vy = v[3]; s.angle = v[4]; s.omega = v[5]; s.fuel = v[6];
-    s.px = v[7]; s.py = v[8]; s.total = v[9];
-    s.status = w[o];
-    s.steps = (int32_t)w[o + 1];
-    s.episode = (int32_t)w[o + 2];
-    s.speed = 0.0;  // (frame() measures the state it produces)
-    s.dist = 0.0;
-}
-
-// quantize (below) and park the result: the next frame's starting state.
-template <typename T, bool kRef = false>
-__device__ __forceinline__ void quantize_park(Lane& s, LaneRecord<T>* rec) {
-    const T v[10] = {(T)s.x, (T)s.y, (T)s.vx, (T)s.vy, (T)s.angle, (T)s.omega, (T)s.fuel, (T)s.px, (T)s.py,
-                     (T)s.total};
-    s.x = v[0]; s.y = v[1]; s.vx = v[2]; s.vy = v[3]; s.angle = v[4]; s.omega = v[5]; s.fuel = v[6];
-    s.total = v[9];
-    if constexpr (!kRef) { s.px = v[7]; s.py = v[8]; }
-    park_lane<T>(rec, v, s.status, s.steps, s.episode);
-}
-
-// frame_checked with the starting state in `rec` (parked) rather than in
-// registers: the fast frame, and for a risky lane the exact frame from the
-// parked state (a wave-uniform rare branch).
-template <bool kRef, bool kFlat, typename T>
-__device__ __forceinline__ double frame_checked_parked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s,
-                                                       const LaneRecord<T>* rec) {
-    bool risky = false;
-    double reward = frame<kRef, kFlat>(k, sw, act, s, &risky);
-    if (__builtin_expect(__ballot(risky) != 0, 0)) {
-        if (risky) {
-            unpark_lane<T>(rec, s);
             reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
         }
     }
@@ -862,6 +622,11 @@ __device__ __forceinline__ void observe(const Consts& k, const Lane& s, float* o
     write_obs_row(v, s.status, o);
 }
 
+// The notebooks' shaped rewards a kernel fuses (kShape): none (the engine's
+// reward only), PPO's calc_reward(state, prev_state) with its two-frame
+// history, REINFORCE's calc_reward(state).
+enum { kShapeNone = 0, kShapePpo = 1, kShapeReinforce = 2 };
+
 // calc_reward(state, prev_state)['total'] of Actor_Critic_PPO.ipynb:164-263
 // (scalers: rl_helpers/scalers.py) on the frame's double observation `v`;
 // prev_dist is prev_state.distance_to_platform, NaN for prev_state None.  The
@@ -891,6 +656,43 @@ __device__ __forceinline__ double notebook_reward(const double v[13], uint32_t s
     const bool landed = status & DD_ST_LANDED, crashed = status & DD_ST_CRASHED;
     const double crash_term = dist > 0.3 ? -200.0 - 100.0 : -200.0;
     total += landed ? 800.0 + fuel * 100.0 : crashed ? crash_term : 0.0;
+    return total;
+}
+
+// calc_reward(state)['total'] of Policy_Gradients.ipynb:162-238 (the REINFORCE
+// notebook; velocity alignment :128-153, scalers rl_helpers/scalers.py) on
+// the frame's double observation `v`.  No prev_state.  The terms are summed
+// in the notebook's order, each formed as the notebook's Python evaluates it
+// (`x**2` as x*x: glibc's pow(x, 2) may differ by an ulp; exp is the device
+// library's): within a few ulps of the notebook's value, as the PPO reward.
+__device__ __forceinline__ double reinforce_reward(const double v[13], uint32_t status) {
+    const double vx = v[2], vy = v[3], angle = v[4], fuel = v[6], dist = v[9], dx = v[10], dy = v[11],
+                 speed = v[12];
+    // time penalty: -inverse_quadratic(dist, decay=50, scaler=1-0.3) - 0.3
+    constexpr double kScale = 1.0 - 0.3;  // (0.7000000000000001, as Python forms it)
+    const double time_penalty = -(kScale * (1.0 / (1.0 + (50.0 * (dist * dist))))) - 0.3;
+    // calc_velocity_alignment: only its sign is used
+    const double odx0 = -dx, ody0 = -dy;
+    const double onorm = sqrt(odx0 * odx0 + ody0 * ody0);
+    const double odx = odx0 / onorm, ody = ody0 / onorm;
+    const double align_v = (vx / speed) * odx + (vy / speed) * ody;
+    const double align = onorm < 1e-6 ? 1.0 : speed < 1e-6 ? 0.0 : align_v;
+    // distance and velocity-alignment terms, only above the platform
+    const bool above = (dist > 0.065) & (dy > 0.0);
+    const double sig = 4.5 * (1.0 / (1.0 + exp(10.0 * (dist - 0.5))));  // scaled_shifted_negative_sigmoid
+    const double distance = above ? ((align > 0.0 ? 1.0 : 0.0) * speed) * sig : 0.0;
+    const double valign = (above & (align > 0.0)) ? 0.5 : 0.0;
+    double total = time_penalty;
+    total += distance;
+    total += valign;
+    const double excess = fabs(angle) - (((0.20 - 0.111) * dist) + 0.111);
+    total += -(excess > 0.0 ? excess : 0.0);
+    const double over = dist < 1 ? speed - 0.1 : speed - 0.4;
+    total += (dist < 1 ? -2.0 : -1.0) * (over > 0.0 ? over : 0.0);
+    total += dy > 0.0 ? 0.0 : dy * 4.0;
+    const bool landed = status & DD_ST_LANDED, crashed = status & DD_ST_CRASHED;
+    const double crash_term = dist > 0.3 ? -200.0 - 100.0 : -200.0;
+    total += landed ? 500.0 + fuel * 100.0 : crashed ? crash_term : 0.0;
     return total;
 }
 

@@ -22,10 +22,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kIn = DD_OBS_DIM;  // 15
-#ifndef DD_MLP_WAVES
-#define DD_MLP_WAVES 8  // per block (one block per CU); experiments try 4 / 12
-#endif
-constexpr int kWaves = DD_MLP_WAVES;
+constexpr int kWaves = 8;  // per block (one block per CU); 12 measured 18.5 -> 22.7 us
 constexpr int kThreads = kWaves * 64;
 constexpr int kCols = 32;  // drones per wave tile
 
@@ -70,13 +67,8 @@ __device__ __forceinline__ f32x4 packed_fragment(const f32x4* src4, int i, uint3
 
 // The three hidden Linears are packed mean-centred over their outputs
 // (policy_mlp.hip weight_at), so the LayerNorm that follows each skips its
-// mean pass (-DDD_MLP_UNCENTERED: the plain weights and the two-pass
-// LayerNorm, for A/B).
-#ifdef DD_MLP_UNCENTERED
-constexpr bool kCentered = false;
-#else
+// mean pass (the plain weights with a two-pass LayerNorm: 18.6 vs 17.6 us).
 constexpr bool kCentered = true;
-#endif
 
 // Hidden row held in register r of accumulator tile t by lane half h
 // (C/D map of the 32x32 MFMAs on gfx950: row = (r&3) + 8(r>>2) + 4h).
@@ -99,20 +91,15 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 // register (exact: the product and the sum are exact, so the one rounding
 // changes nothing): v_cvt_pk_f16_f32, v_pk_mul_f32, two v_fma_mix_f32,
 // v_cvt_pk_f16_f32 = 5 VALU per pair, the same bits as converting hi back to
-// f32 and subtracting (6; -DDD_MLP_SPLIT_CVT, tools/mlp_equal_check.py).
+// f32 and subtracting (6; tools/mlp_equal_check.py).
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
     uint32_t hp = __builtin_bit_cast(uint32_t, f16x2{(_Float16)a, (_Float16)b});
     asm("" : "+v"(hp));  // widen hi from the packed register (else each half is converted twice)
-#ifdef DD_MLP_SPLIT_CVT
-    const f16x2 h = __builtin_bit_cast(f16x2, hp);
-    const f32x2 r = (f32x2{a, b} - f32x2{(float)h.x, (float)h.y}) * f32x2{kLoScale, kLoScale};
-#else
     const f32x2 as = f32x2{a, b} * f32x2{kLoScale, kLoScale};
     f32x2 r;
     asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r.x) : "v"(hp), "v"(kLoScale), "v"(as.x));
     asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r.y) : "v"(hp), "v"(kLoScale),
         "v"(as.y));
-#endif
     const f16x2 l = {(_Float16)r.x, (_Float16)r.y};
     hi = hp;
     lo = __builtin_bit_cast(uint32_t, l);
@@ -235,13 +222,9 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
             q2 = __builtin_elementwise_fma(d, d, q2);
         }
     const float sq = add_other_half(q2.x + q2.y);
-#ifdef DD_MLP_IEEE_RSTD  // correctly rounded 1 / sqrt (~30 VALU: IEEE sqrt + division), A/B switch
-    const float rstd = 1.0f / sqrtf(sq / (float)kRows + eps);
-#else
     // v_rsq_f32 (1 ulp), what torch's LayerNorm kernels use (rsqrtf), instead
     // of an IEEE sqrt and division: ~28 fewer VALU per LayerNorm
     const float rstd = __builtin_amdgcn_rsqf(sq / (float)kRows + eps);
-#endif
     const f32x2 rs2 = {rstd, rstd}, nb2 = {-rstd * mean, -rstd * mean};
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -276,17 +259,6 @@ __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* 
 template <int NT>
 __device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                 f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
-#ifdef DD_MLP_PAD  // timing-only: DD_MLP_PAD extra packed f32 FMAs (8 chains) per split layer, the VALU-cost slope
-    {
-        f32x2 pz[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) pz[q] = f32x2{acc[0][q], acc[0][q + 8]};
-#pragma unroll
-        for (int q = 0; q < DD_MLP_PAD; ++q) asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(pz[q & 7]));
-#pragma unroll
-        for (int q = 0; q < 8; ++q) asm volatile("" ::"v"(pz[q]));
-    }
-#endif
     norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
         split8(&v[0], bh[2 * t], bl[2 * t]);
         split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
@@ -358,14 +330,10 @@ __device__ __forceinline__ void layer16_hihi(const u32x4* __restrict__ a16, int 
 // agree to float32 rounding.)
 __device__ __forceinline__ float bernoulli_logp(float p, bool on) {
     const float pc = fminf(fmaxf(p, FLT_EPSILON), 1.0f - FLT_EPSILON);
-#ifdef DD_MLP_LOG1P  // A/B: both logs evaluated per factor (a select of logf and log1pf)
-    return on ? logf(pc) : log1pf(-pc);
-#else
     // one logf per factor: log(1 - p) with 1 - p rounded once (exact for p >= 1/2,
     // else within 2^-24 of log1p(-p)) instead of a select between logf and
     // log1pf, which evaluated both (~90 VALU per 32-drone tile)
     return logf(on ? pc : 1.0f - pc);
-#endif
 }
 
 
@@ -413,12 +381,7 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
         norm_relu_split<4>(acc4, lds + kV1, eps, h, bh, bl);
         mid();
         layer16<4, 8>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
-#ifdef DD_MLP_SERIAL  // A/B: the serial schedule everywhere
-        constexpr bool kPipelined = false;
-#else
-        constexpr bool kPipelined = kPipe;
-#endif
-        if constexpr (kPipelined) {
+        if constexpr (kPipe) {
             norm_split_cross<2>(acc4, lds + kV2, eps, h, a16 + kA3 / 4, lane, bh, bl, acc2);
             layer16_hihi<2, 8>(a16 + kA3 / 4, lane, bh, acc2, lds + kV3 + 4 * h);
         } else {  // layer 2's LayerNorm + split, then all of layer 3
@@ -440,133 +403,6 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
     }
     __builtin_amdgcn_sched_barrier(0);
     head_of<K>(lds, h, y3, z);
-}
-
-// ---- Two tiles per wave (f16x3): one tile's MFMAs against the other's VALU --
-// A gfx950 SIMD overlaps a wave's VALU with that wave's own earlier,
-// independent MFMAs, never with another wave's ("What the
-// actor's time is made of").  With one tile per wave nearly every VALU
-// instruction waits for the MFMAs just before it, so a tile costs its VALU
-// plus its MFMA time.  mlp_pair runs two tiles (A, B) in one wave, half a
-// layer apart:
-//   L1(A) | L1(B) + LN1(A) | L2(A) + LN1(B) | L2(B) + LN2(A) | L3(A) + LN2(B) |
-//   L3(B) + LN3(A) + head(A) | LN3(B) + head(B)
-// and inside each phase the one tile's MFMAs are issued one by one between
-// slices of the other tile's LayerNorm / split (sched_group_barrier), so the
-// VALU runs in the MFMA pipe's shadow.  Every accumulator sees the same MFMAs
-// in the same order as layer16's, and the LayerNorm / split / head are the same
-// code (mlp_body's), so both tiles come out bit for bit as mlp_body's.
-
-// layer16 without its scheduling fences (the phase's interleave orders it)
-template <int NT, int KS>
-__device__ __forceinline__ void layer16_free(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
-                                             const f16x8 (&bl)[KS], f32x16 (&acc)[NT], const float* bias_h) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const u32x4* blk = a16 + (t * KS + s) * 128;
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, blk[lane]), bl[s], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, blk[64 + lane]), bh[s], acc[t], 0,
-                                                            0, 0);
-        }
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a16[(t * KS + s) * 128 + lane]),
-                                                            bh[s], acc[t], 0, 0, 0);
-}
-
-#ifndef DD_MLP_PAIR_VALU
-#define DD_MLP_PAIR_VALU 4  // VALU instructions placed after each MFMA of a phase (lab knob)
-#endif
-
-// The interleave of one phase: NM times (one MFMA, then up to NV VALU).
-template <int NM, int NV>
-__device__ __forceinline__ void interleave_mfma_valu() {
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);  // VALU
-    }
-}
-
-template <int NT>
-__device__ __forceinline__ void norm_split_free(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
-                                                f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
-    auto emit = [&](int t, const float (&v)[16]) {
-        split8(&v[0], bh[2 * t], bl[2 * t]);
-        split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
-    };
-    norm_relu_emit<NT, decltype(emit), false>(acc, vec, eps, h, emit);
-}
-
-template <int NT>
-__device__ __forceinline__ void norm_free(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
-                                          float (&y)[NT][16]) {
-    auto emit = [&](int t, const float (&v)[16]) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) y[t][r] = v[r];
-    };
-    norm_relu_emit<NT, decltype(emit), false>(acc, vec, eps, h, emit);
-}
-
-// Two tiles' networks (f16x3) up to the last layer's outputs: lane (c, h)
-// holds column c's inputs xa / xb as mlp_body's kSplit path; za / zb as its z.
-template <int K, typename Mid = NoMid>
-__device__ __forceinline__ void mlp_pair(const float* lds, int lane, const float (&xa)[8], const float (&xb)[8],
-                                         float (&za)[K], float (&zb)[K], Mid mid = {}) {
-    constexpr int NV = DD_MLP_PAIR_VALU;
-    const u32x4* a16 = reinterpret_cast<const u32x4*>(lds);
-    const int h = lane >> 5;
-    const float eps = lds[kB4 + 3];
-    f32x16 accA[4], accB[4], acc2A[2], acc2B[2];
-    f16x8 bhA[8], blA[8], bhB[8], blB[8];
-    float y3A[2][16], y3B[2][16];
-    {
-        f16x8 ih[1], il[1];
-        split8(xa, ih[0], il[0]);
-        layer16_free<4, 1>(a16 + kA1 / 4, lane, ih, il, accA, lds + kV1 + 4 * h);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    {
-        f16x8 ih[1], il[1];
-        split8(xb, ih[0], il[0]);
-        layer16_free<4, 1>(a16 + kA1 / 4, lane, ih, il, accB, lds + kV1 + 4 * h);
-        norm_split_free<4>(accA, lds + kV1, eps, h, bhA, blA);
-        interleave_mfma_valu<12, NV>();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mid();
-    __builtin_amdgcn_sched_barrier(0);
-    layer16_free<4, 8>(a16 + kA2 / 4, lane, bhA, blA, accA, lds + kV2 + 4 * h);
-    norm_split_free<4>(accB, lds + kV1, eps, h, bhB, blB);
-    interleave_mfma_valu<96, NV>();
-    __builtin_amdgcn_sched_barrier(0);
-    layer16_free<4, 8>(a16 + kA2 / 4, lane, bhB, blB, accB, lds + kV2 + 4 * h);
-    norm_split_free<4>(accA, lds + kV2, eps, h, bhA, blA);
-    interleave_mfma_valu<96, NV>();
-    __builtin_amdgcn_sched_barrier(0);
-    layer16_free<2, 8>(a16 + kA3 / 4, lane, bhA, blA, acc2A, lds + kV3 + 4 * h);
-    norm_split_free<4>(accB, lds + kV2, eps, h, bhB, blB);
-    interleave_mfma_valu<48, NV>();
-    __builtin_amdgcn_sched_barrier(0);
-    layer16_free<2, 8>(a16 + kA3 / 4, lane, bhB, blB, acc2B, lds + kV3 + 4 * h);
-    norm_free<2>(acc2A, lds + kV3, eps, h, y3A);
-    head_of<K>(lds, h, y3A, za);
-    interleave_mfma_valu<48, NV>();
-    __builtin_amdgcn_sched_barrier(0);
-    norm_free<2>(acc2B, lds + kV3, eps, h, y3B);
-    head_of<K>(lds, h, y3B, zb);
 }
 
 // The actor's head: Sigmoid probabilities of the last layer's outputs.

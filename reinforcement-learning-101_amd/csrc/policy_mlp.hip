@@ -227,93 +227,15 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
         const int64_t d = tile * kCols + c;  // this lane's drone (column)
         const bool live = d < p.n;
         float z[K];
-#ifdef DD_EXP_MLP_NOCOMPUTE  // timing-only: the launch, the parameter image and the outputs, no network
-        mid();
-#pragma unroll
-        for (int k = 0; k < K; ++k) z[k] = x[k] + lds[kB4 + k];
-#else
         mlp_body<K, kSplit>(lds, lane, x, z, mid);
-#endif
         if (!live || h != 0) continue;
         emit_outputs<K>(p, d, z);
     }
     mid();  // a wave without a tile still takes its part in the second barrier
 }
 
-// DD_MLP_F16X3 with two tiles per wave (mlp_core.h mlp_pair): blocks of 4
-// waves, one per SIMD, one block per CU; a wave owns the pair of tiles
-// (2q, 2q + 1), i.e. 64 consecutive drones.  Same LDS image and prologue as
-// mlp_kernel.  -DDD_MLP_PAIR=0 keeps mlp_kernel for f16x3 (A/B).
-#ifndef DD_MLP_PAIR
-#define DD_MLP_PAIR 0
-#endif
-constexpr int kPairWaves = 4;
-constexpr int kPairThreads = kPairWaves * 64;
-
-template <int K>
-__global__ __launch_bounds__(kPairThreads, 1) void mlp_pair_kernel(const float* __restrict__ packed, FwdArgs p) {
-    extern __shared__ f32x4 lds4[];
-    const float* lds = reinterpret_cast<const float*>(lds4);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
-    const int64_t pairs = (p.n + 2 * kCols - 1) / (2 * kCols);
-    int64_t pair = (int64_t)blockIdx.x * kPairWaves + wave;
-    float xa[8], xb[8];
-    load_inputs<true>(p, 2 * pair, lane, xa);
-    load_inputs<true>(p, 2 * pair + 1, lane, xb);
-    const f32x4* src4 = reinterpret_cast<const f32x4*>(packed);
-    for (int i = threadIdx.x; i < kA2 / 4; i += kPairThreads) lds4[i] = src4[i];
-    for (int i = kV1 / 4 + threadIdx.x; i < kPacked / 4; i += kPairThreads)
-        lds4[i] = packed_fragment(src4, i, pack_tag(DD_MLP_F16X3, K));
-    asm volatile("" ::"v"(xa[0]), "v"(xa[1]), "v"(xa[2]), "v"(xa[3]), "v"(xa[4]), "v"(xa[5]), "v"(xa[6]), "v"(xa[7]),
-                 "v"(xb[0]), "v"(xb[1]), "v"(xb[2]), "v"(xb[3]), "v"(xb[4]), "v"(xb[5]), "v"(xb[6]), "v"(xb[7]));
-    constexpr int kChunk = 64 * 4;
-    for (int q = wave; q < (kV1 - kA2) / kChunk; q += kPairWaves) {
-        const int off = kA2 + q * kChunk;
-        __builtin_amdgcn_global_load_lds(packed + off + lane * 4, lds4 + off / 4, 16, 0, 0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    bool first = true;
-    const auto mid = [&first] {
-        if (first) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            first = false;
-        }
-    };
-    for (; pair < pairs; pair += (int64_t)gridDim.x * kPairWaves) {
-        if (!first) {
-            load_inputs<true>(p, 2 * pair, lane, xa);
-            load_inputs<true>(p, 2 * pair + 1, lane, xb);
-        }
-        float za[K], zb[K];
-        mlp_pair<K>(lds, lane, xa, xb, za, zb, mid);
-        if (h != 0) continue;
-        const int64_t da = 2 * pair * kCols + c, db = da + kCols;
-        if (da < p.n) emit_outputs<K>(p, da, za);
-        if (db < p.n) emit_outputs<K>(p, db, zb);
-    }
-    mid();  // a wave without a pair still takes its part in the second barrier
-}
-
-template <int K>
-hipError_t launch_pair(const float* packed, const FwdArgs& a, hipStream_t s) {
-    const hipError_t e = hipFuncSetAttribute((const void*)mlp_pair_kernel<K>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
-    if (e != hipSuccess) return e;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const int64_t pairs = (a.n + 2 * kCols - 1) / (2 * kCols);
-    const int64_t want = (pairs + kPairWaves - 1) / kPairWaves;
-    const unsigned blocks = (unsigned)(want < cus ? want : cus);
-    hipLaunchKernelGGL((mlp_pair_kernel<K>), dim3(blocks), dim3(kPairThreads), kLdsBytes, s, packed, a);
-    return hipGetLastError();
-}
-
 template <int K, bool kSplit>
 hipError_t launch(const float* packed, const FwdArgs& a, hipStream_t s) {
-    if constexpr (kSplit && DD_MLP_PAIR) return launch_pair<K>(packed, a, s);
     // the LDS image exceeds the 64 KB default; the attribute is per device, so
     // it is set on every launch (a cheap host call) rather than once per process
     const hipError_t e = hipFuncSetAttribute((const void*)mlp_kernel<K, kSplit>,

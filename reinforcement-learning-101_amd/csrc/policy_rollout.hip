@@ -5,7 +5,9 @@
 //                       probs  = actor(obs[k])                   :851-855
 //                       a, lp  = Bernoulli(probs).sample / .log_prob(a).sum   :857-859
 //                       reward[k], done[k] = DroneGame.step(a)   (game_engine.py:95-138,
-//                                            notebook reward + max_steps optional)
+//                                            notebook reward + max_steps optional:
+//                                            PPO's, or REINFORCE's for collect_episodes,
+//                                            Policy_Gradients.ipynb:528-598)
 //
 // The two kernels it replaces (dd_mlp_forward + dd_step per frame) each pay a
 // launch, the actor re-reads its 111 KB of packed parameters into every CU's
@@ -67,6 +69,7 @@ struct Args {
     int64_t n;
     int32_t frames;
     int32_t max_steps;
+    int32_t shape;         // kShapeNone / kShapePpo / kShapeReinforce (frame.h)
     int32_t rows_aligned;  // every frame's obs rows start 16-byte aligned (obs aligned, n % 4 == 0)
     int32_t final_aligned; // obs_final 16-byte aligned
 };
@@ -140,7 +143,8 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     constexpr bool kGuard = !kRef && std::is_same<T, double>::value;
-    const bool shaped = p.shaped_hist != nullptr;
+    const bool shaped = p.shape != kShapeNone;
+    const bool ppo = p.shape == kShapePpo;
     const int64_t env = a.env_id_base + d;
 
     Lane s;
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
     s.fuel = a.fuel[d]; s.px = a.px[d]; s.py = a.py[d]; s.total = a.total[d];
     s.status = a.status[d]; s.steps = a.steps[d]; s.episode = a.episode[d];
     double h0 = 0.0, h1 = 0.0;  // the notebook reward's two-frame distance history
-    if (shaped) { h0 = p.shaped_hist[d]; h1 = p.shaped_hist[p.n + d]; }
+    if (ppo) { h0 = p.shaped_hist[d]; h1 = p.shaped_hist[p.n + d]; }
     float x[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
         }
         T* rew = reinterpret_cast<T*>(p.reward) + fo + d;
         uint8_t* dn = p.done + fo + d;
-        if (shaped) {  // dd_step's notebook path with the history in h0 / h1
+        if (shaped) {  // dd_step's notebook path (PPO: the history in h0 / h1)
             double v[13];
             observe_values<kGuard, true>(k, s, v);  // the notebook reward's doubles: exact quotients
             double sr = 0.0;
@@ -204,12 +208,16 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
             } else if (was_done) {
                 sd = true;
             } else {
-                const bool odd = (s.steps & 1) != 0;
-                sr = notebook_reward(v, s.status, odd ? h1 : h0);
-                h1 = odd ? v[9] : h1;
-                h0 = odd ? h0 : v[9];
+                if (ppo) {
+                    const bool odd = (s.steps & 1) != 0;
+                    sr = notebook_reward(v, s.status, odd ? h1 : h0);
+                    h1 = odd ? v[9] : h1;
+                    h0 = odd ? h0 : v[9];
+                } else {
+                    sr = reinforce_reward(v, s.status);
+                }
                 sd = (s.status & DD_ST_DONE) != 0;
-                if (p.max_steps > 0 && s.steps >= p.max_steps) {  // collect_episodes_ppo timeout
+                if (p.max_steps > 0 && s.steps >= p.max_steps) {  // the collection loops' timeout
                     sr = (s.status & DD_ST_LANDED) ? sr : sr - 500;
                     sd = true;
                     s.status |= DD_ST_DONE;
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(kThreads) void policy_rollout_kernel(const float* _
         a.x[d] = (T)s.x; a.y[d] = (T)s.y; a.vx[d] = (T)s.vx; a.vy[d] = (T)s.vy; a.angle[d] = (T)s.angle;
         a.omega[d] = (T)s.omega; a.fuel[d] = (T)s.fuel; a.px[d] = (T)s.px; a.py[d] = (T)s.py;
         a.total[d] = (T)s.total; a.status[d] = (uint8_t)s.status; a.steps[d] = s.steps; a.episode[d] = s.episode;
-        if (shaped) { p.shaped_hist[d] = h0; p.shaped_hist[p.n + d] = h1; }
+        if (ppo) { p.shaped_hist[d] = h0; p.shaped_hist[p.n + d] = h1; }
     }
 }
 
@@ -266,7 +274,10 @@ extern "C" int dd_policy_rollout(const DDConfig* cfg, const DDState* st, const f
     if (!cfg || !io || !dd::state_ok(st) || n < 0 || io->frames < 0) return hipErrorInvalidValue;
     if (compute != DD_MLP_F32 && compute != DD_MLP_F16X3) return hipErrorInvalidValue;
     if ((io->engine_reward == nullptr) != (io->engine_done == nullptr)) return hipErrorInvalidValue;
-    if (io->engine_reward && !io->shaped_hist) return hipErrorInvalidValue;
+    if (io->shaped_mode != DD_SHAPED_PPO && io->shaped_mode != DD_SHAPED_REINFORCE) return hipErrorInvalidValue;
+    const int shape = io->shaped_mode == DD_SHAPED_REINFORCE ? dd::kShapeReinforce
+                      : io->shaped_hist ? dd::kShapePpo : dd::kShapeNone;
+    if (io->engine_reward && shape == dd::kShapeNone) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
     if (!packed || !io->obs0 || (io->frames > 0 && (!io->reward || !io->done))) return hipErrorInvalidValue;
     if (reinterpret_cast<uintptr_t>(packed) & 15u) return hipErrorInvalidValue;  // read as 16-byte fragments
@@ -288,6 +299,7 @@ extern "C" int dd_policy_rollout(const DDConfig* cfg, const DDState* st, const f
     p.n = n;
     p.frames = io->frames;
     p.max_steps = io->max_steps;
+    p.shape = shape;
     p.rows_aligned = (reinterpret_cast<uintptr_t>(io->obs) & 15u) == 0 && (n & 3) == 0;
     p.final_aligned = (reinterpret_cast<uintptr_t>(io->obs_final) & 15u) == 0;
     const bool ref = dd::uses_reference_physics(*cfg);

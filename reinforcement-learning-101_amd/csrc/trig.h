@@ -48,15 +48,9 @@ constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-
                  C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                  C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
 
-// Horner step a + z * b; fused unless DD_TRIG_NO_FMA (the polynomial tails
-// are far below an ulp of the result, so fusing only removes roundings).
-DD_HD inline double hstep(double a, double z, double b) {
-#ifdef DD_TRIG_NO_FMA
-    return a + z * b;
-#else
-    return fma(z, b, a);
-#endif
-}
+// Horner step a + z * b, fused (the polynomial tails are far below an ulp of
+// the result, so fusing only removes roundings).
+DD_HD inline double hstep(double a, double z, double b) { return fma(z, b, a); }
 
 // The same Horner step with the constant `a` as an SGPR operand of a VOP3
 // v_fma_f64 (device code, kSgpr).  Left to itself the compiler materialises
@@ -67,7 +61,7 @@ DD_HD inline double hstep(double a, double z, double b) {
 // chain (two constants) keeps the plain form: a VOP3 reads one SGPR pair.
 template <bool kSgpr>
 DD_HD inline double hstep_c(double a, double z, double b) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(DD_TRIG_NO_FMA)
+#if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (kSgpr) {
         double r;
         asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(z), "v"(b), "s"(a));

@@ -16,17 +16,23 @@ __all__ = [
     "DD_F32", "DD_F64", "DD_ACT_BITMASK", "DD_ACT_F32X3", "DD_ACT_U8X3", "DD_ACT_PHILOX",
     "DD_ST_DONE", "DD_ST_LANDED", "DD_ST_CRASHED", "DD_ST_PLAT_LEFT", "DD_OBS_DIM",
     "DD_RENDER_HUD", "DD_RENDER_GAME_OVER", "DD_MLP_F32", "DD_MLP_F16X3",
+    "DD_SHAPED_PPO", "DD_SHAPED_REINFORCE", "DD_ROLLOUT_AUTO", "DD_ROLLOUT_SINGLE", "DD_ROLLOUT_SPLIT_NO_WAIT",
+    "DD_ROLLOUT_FLUSHED", "DD_ROLLOUT_HELD", "DD_ROLLOUT_SPLIT", "DD_ERR_HANDOVER",
     "DDConfig", "DDState", "DDStepIO", "DDRolloutIO", "DDMlpParams", "DDMlpIO", "DDPolicyRolloutIO", "lib", "load", "library_path", "check",
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 10
+DD_ABI_VERSION = 11
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
 DD_OBS_DIM = 15
 DD_RENDER_HUD, DD_RENDER_GAME_OVER = 1, 2
 DD_MLP_F32, DD_MLP_F16X3 = 0, 1
+DD_SHAPED_PPO, DD_SHAPED_REINFORCE = 0, 1
+DD_ROLLOUT_AUTO, DD_ROLLOUT_SINGLE, DD_ROLLOUT_SPLIT_NO_WAIT = 0, 1, 2
+DD_ROLLOUT_FLUSHED, DD_ROLLOUT_HELD, DD_ROLLOUT_SPLIT = 16, 17, 18
+DD_ERR_HANDOVER = 1
 
 _D = ctypes.c_double
 _I = ctypes.c_int32
@@ -79,7 +85,7 @@ class DDStepIO(ctypes.Structure):
         ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("obs", ctypes.c_void_p),
         ("done_idx", ctypes.c_void_p), ("done_count", ctypes.c_void_p),
         ("shaped_hist", ctypes.c_void_p), ("shaped_reward", ctypes.c_void_p), ("shaped_done", ctypes.c_void_p),
-        ("max_steps", _I), ("_pad2", _I), ("state_out", ctypes.c_void_p),
+        ("max_steps", _I), ("shaped_mode", _I), ("state_out", ctypes.c_void_p),
     ]
 
 
@@ -89,7 +95,7 @@ class DDRolloutIO(ctypes.Structure):
         ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p), ("obs", ctypes.c_void_p),
         ("action_seed", ctypes.c_uint64), ("action_step", ctypes.c_int64),
         ("shaped_hist", ctypes.c_void_p), ("engine_reward", ctypes.c_void_p), ("engine_done", ctypes.c_void_p),
-        ("max_steps", _I), ("reserved", _I),
+        ("max_steps", _I), ("shaped_mode", _I), ("kernel", _I), ("_pad", _I),
     ]
 
 
@@ -114,6 +120,7 @@ class DDPolicyRolloutIO(ctypes.Structure):
         ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p),
         ("seed", ctypes.c_uint64), ("step", ctypes.c_int64), ("frames", _I), ("max_steps", _I),
         ("shaped_hist", ctypes.c_void_p), ("engine_reward", ctypes.c_void_p), ("engine_done", ctypes.c_void_p),
+        ("shaped_mode", _I), ("_pad", _I),
     ]
 
 
@@ -124,6 +131,9 @@ EXPORTS = {
                                ctypes.POINTER(DDStepIO), ctypes.c_int64, ctypes.c_void_p]),
     "dd_rollout": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState),
                                   ctypes.POINTER(DDRolloutIO), ctypes.c_int64, ctypes.c_void_p]),
+    "dd_rollout_kernel": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState),
+                                         ctypes.POINTER(DDRolloutIO), ctypes.c_int64]),
+    "dd_device_errors": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), _I]),
     "dd_reset": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "dd_shaped_reset": (ctypes.c_int, [ctypes.POINTER(DDConfig), ctypes.POINTER(DDState), ctypes.c_void_p,
@@ -155,7 +165,7 @@ EXPORTS = {
 
 #: symbols a timing-only lab build (tools/build_variants.sh) or an older
 #: committed source built for an A/B run may lack
-_LAB_OPTIONAL = ("dd_build_info", "dd_selftest_sqrt")
+_LAB_OPTIONAL = ("dd_build_info", "dd_selftest_sqrt", "dd_rollout_kernel", "dd_device_errors")
 
 
 class NativeLibraryError(RuntimeError):

@@ -10,6 +10,7 @@ the CPU.
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import Dict, List, Optional, Tuple
 
@@ -71,11 +72,13 @@ def gather_state(fields: Dict[str, torch.Tensor], total: int, dst: int = 0, grou
     field: the consumer-side twin of the step path's shards (checkpoints,
     a learner that needs the whole batch)."""
     groups: Dict[torch.dtype, List[str]] = {}
-    for name, t in fields.items():
-        groups.setdefault(t.dtype, []).append(name)
+    for name in sorted(fields):  # the same column order on every rank, whatever the dict order
+        groups.setdefault(fields[name].dtype, []).append(name)
     out: Dict[str, torch.Tensor] = {}
-    for dtype, names in groups.items():
-        cols = [fields[n].reshape(fields[n].shape[0], -1) for n in names]
+    for dtype in sorted(groups, key=str):
+        names = groups[dtype]
+        # reshape(count, prod(rest)), not (count, -1): a rank may hold zero rows
+        cols = [fields[n].reshape(fields[n].shape[0], math.prod(fields[n].shape[1:])) for n in names]
         widths = [c.shape[1] for c in cols]
         g = gather_obs(torch.cat(cols, dim=1), total, dst=dst, group=group)
         if g is None:

@@ -456,6 +456,63 @@ def gae_set(seed=5, T=257, cols=48, gamma=0.99, lam=0.95) -> dict:
                 gamma=np.float64(gamma), lam=np.float64(lam))
 
 
+# The REINFORCE notebook's reward (the widening of SURVEY §8(f) row 1)
+def reinforce_reward_fn():
+    """calc_reward from Policy_Gradients.ipynb (REINFORCE), executed from the
+    notebook's own cells (calc_velocity_alignment :128-153, calc_reward
+    :162-238) with rl_helpers/scalers.py; read at generation time, nothing is
+    copied."""
+    import json as _json
+    import math
+    from types import SimpleNamespace
+    from delivery_drone.game.socket_client import DroneState
+    import rl_helpers.scalers as scalers
+    nb = _json.load(open(os.path.join(REF, "Policy_Gradients.ipynb")))
+    ns = {"np": np, "math": math, "DroneState": DroneState}
+    ns.update({k: getattr(scalers, k) for k in dir(scalers) if not k.startswith("_")})
+    for cell in nb["cells"]:
+        src = "".join(cell["source"])
+        if cell["cell_type"] == "code" and ("def calc_velocity_alignment" in src or "def calc_reward" in src):
+            exec(compile(src, "Policy_Gradients.ipynb", "exec"), ns)
+    calc = ns["calc_reward"]
+    return lambda state_dict: calc(SimpleNamespace(**state_dict))
+
+
+def reinforce_set(rng, counts: dict, max_steps: int = 300) -> dict:
+    """Single steps whose next_state goes through the REINFORCE notebook's
+    calc_reward, with step counts around max_steps for collect_episodes'
+    timeout (Policy_Gradients.ipynb:590-593: -500 unless landed, done)."""
+    reward = reinforce_reward_fn()
+    ins = {}
+    for kind, m in counts.items():
+        for k, v in draw_states(rng, m, kind).items():
+            ins.setdefault(k, []).append(v)
+    ins = {k: np.concatenate(v) for k, v in ins.items()}
+    n = ins["x"].shape[0]
+    ins["done"][:] = False
+    ins["steps"] = np.where(rng.random(n) < 0.3, rng.integers(max_steps - 3, max_steps + 2, n),
+                            rng.integers(0, max_steps - 3, n)).astype(np.int32)
+    g = new_game()
+    out_total, out_shaped, out_done = [], [], []
+    for i in range(n):
+        s = {k: (v[i].item() if hasattr(v[i], "item") else v[i]) for k, v in ins.items()}
+        poke(g, s)
+        st, _, done, _ = g.step(act_dict(int(ins["action"][i])))
+        tot = reward(st)["total"]
+        shaped, sdone = tot, bool(done)
+        if g.steps >= max_steps:
+            if not st["landed"]:
+                shaped -= 500
+            sdone = True
+        out_total.append(tot)
+        out_shaped.append(shaped)
+        out_done.append(sdone)
+    rec = {f"in_{k}": np.asarray(v) for k, v in ins.items()}
+    rec.update(max_steps=np.int32(max_steps), out_total=np.asarray(out_total),
+               out_shaped=np.asarray(out_shaped), out_shaped_done=np.asarray(out_done))
+    return rec
+
+
 # The notebooks' policy / value networks (SURVEY §8(f) row 2)
 def policy_set(seed=11, games=24, frames=120) -> dict:
     """DroneGamerBoi / DroneTeacherBoi of Actor_Critic_PPO.ipynb:376-424,
@@ -482,6 +539,9 @@ def policy_set(seed=11, games=24, frames=120) -> dict:
     critic.load_state_dict(torch.load(os.path.join(mdir, "drone_critic_v1.pth"), map_location="cpu",
                                       weights_only=True))
     rng = np.random.default_rng(seed)
+    # DroneGame.reset draws its spawns from numpy's global RNG (game_engine.py:66-85):
+    # seeded here so that the fixture regenerates byte for byte
+    np.random.seed(seed)
     rows = []
     for g in range(games):
         game = new_game(randomize_drone=True, randomize_platform=True)
@@ -511,10 +571,25 @@ def policy_set(seed=11, games=24, frames=120) -> dict:
 
 
 def main():
-    if sys.argv[1:] == ["--only", "policy"]:
-        np.savez_compressed(os.path.join(HERE, "policy.npz"), **policy_set())
-        print("policy fixture written to", HERE)
+    out = HERE
+    args = sys.argv[1:]
+    if args[:1] == ["--out"]:  # regenerate into another directory (tests/test_golden_regen.py)
+        out, args = args[1], args[2:]
+    only = {"policy": lambda: np.savez_compressed(os.path.join(out, "policy.npz"), **policy_set()),
+            "reinforce": lambda: np.savez_compressed(os.path.join(out, "reinforce_reward.npz"),
+                                                     **reinforce_set(np.random.default_rng(991),
+                                                                     REINFORCE_COUNTS))}
+    if args[:1] == ["--only"]:
+        only[args[1]]()
+        print(f"{args[1]} fixture written to", out)
         return
+    write_all(out)
+
+
+REINFORCE_COUNTS = {"broad": 1200, "pad": 1200, "ground": 400, "bounds": 200}
+
+
+def write_all(HERE):
     rng = np.random.default_rng(20261015)
     kats = notebook_kats()
     with open(os.path.join(HERE, "kat_notebooks.json"), "w") as f:
@@ -542,6 +617,8 @@ def main():
     np.savez_compressed(os.path.join(HERE, "shaped_reward.npz"),
                         **shaped_set(np.random.default_rng(777), {"broad": 1200, "pad": 1200, "ground": 400,
                                                                  "bounds": 200}))
+    np.savez_compressed(os.path.join(HERE, "reinforce_reward.npz"),
+                        **reinforce_set(np.random.default_rng(991), REINFORCE_COUNTS))
     np.savez_compressed(os.path.join(HERE, "gae.npz"), **gae_set())
     np.savez_compressed(os.path.join(HERE, "policy.npz"), **policy_set())
     print("fixtures written to", HERE)

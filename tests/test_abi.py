@@ -115,19 +115,55 @@ def test_argument_errors_return_invalid_value_without_gpu():
     rio.engine_done = 8
     assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
     rio.engine_reward = rio.engine_done = None
+    rio.shaped_mode = 2  # DD_SHAPED_PPO or DD_SHAPED_REINFORCE
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.shaped_mode = abi.DD_SHAPED_REINFORCE  # engine outputs next to the REINFORCE reward: fine
+    rio.kernel = 3  # DD_ROLLOUT_AUTO / _SINGLE / _SPLIT_NO_WAIT
+    assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == EINVAL
+    rio.kernel = abi.DD_ROLLOUT_AUTO
+    rio.shaped_mode = abi.DD_SHAPED_PPO
     rio.frames = 0  # nothing to do
     assert lib.dd_rollout(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(rio), 4, None) == 0
     io.done_idx = None
     io.action_format = 3  # Philox actions are rollout-only
     assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
+    io.action_format = 0
+    io.shaped_reward = 8  # PPO mode: the three shaped pointers together or none
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
+    io.shaped_mode = abi.DD_SHAPED_REINFORCE  # REINFORCE: reward and done, no history
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
+    io.shaped_mode = 5
+    io.shaped_done = 8
+    assert lib.dd_step(ctypes.byref(cfg), ctypes.byref(_state()), ctypes.byref(io), 4, None) == EINVAL
     assert lib.dd_error_string(EINVAL)
+
+
+def test_rollout_kernel_choice_without_gpu():
+    """dd_rollout_kernel names the kernel dd_rollout would launch (host logic
+    only; the split kernel needs the device's CU count, so it is not chosen
+    here)."""
+    lib = abi.lib()
+    cfg = EnvConfig().to_abi()
+    rio = abi.DDRolloutIO()
+    rio.frames, rio.reward, rio.done = 4, 8, 8
+    rio.action_format = abi.DD_ACT_PHILOX
+    st = _state()
+    assert lib.dd_rollout_kernel(ctypes.byref(cfg), ctypes.byref(st), ctypes.byref(rio), 8) == abi.DD_ROLLOUT_HELD
+    rio.obs = 16 + 4  # rows not 16-byte aligned: the flushed path
+    assert lib.dd_rollout_kernel(ctypes.byref(cfg), ctypes.byref(st), ctypes.byref(rio), 8) == abi.DD_ROLLOUT_FLUSHED
+    assert lib.dd_rollout_kernel(ctypes.byref(cfg), ctypes.byref(st), ctypes.byref(rio), 6) == abi.DD_ROLLOUT_FLUSHED
+    assert lib.dd_rollout_kernel(None, ctypes.byref(st), ctypes.byref(rio), 8) == -1
+    assert lib.dd_rollout_kernel(ctypes.byref(cfg), ctypes.byref(st), ctypes.byref(rio), 0) == -1
+    assert lib.dd_device_errors(None, 0) == 1  # EINVAL: no output
 
 
 def test_policy_rollout_argument_errors_without_gpu():
     lib = abi.lib()
     cfg = EnvConfig().to_abi()
     EINVAL = 1
-    assert ctypes.sizeof(abi.DDPolicyRolloutIO) == 7 * 8 + 8 + 8 + 4 + 4 + 3 * 8  # the C struct's layout
+    assert ctypes.sizeof(abi.DDPolicyRolloutIO) == 7 * 8 + 8 + 8 + 4 + 4 + 3 * 8 + 8  # the C struct's layout
+    assert ctypes.sizeof(abi.DDRolloutIO) == 8 + 8 + 3 * 8 + 8 + 8 + 3 * 8 + 4 * 4
+    assert ctypes.sizeof(abi.DDStepIO) == 8 + 8 + 5 * 8 + 3 * 8 + 8 + 8
     io = abi.DDPolicyRolloutIO()
     io.obs0 = io.reward = io.done = 8
     io.frames = 4

@@ -26,10 +26,10 @@ def bits_equal(a, b):
     return torch.equal(a, b)
 
 
-def notebook_twins(n, dev, precision, max_steps, **cfg):
+def notebook_twins(n, dev, precision, max_steps, mode="notebook", **cfg):
     c = EnvConfig(**cfg)
-    a = VecDroneEnv(n, device=dev, config=c, precision=precision, reward_mode="notebook", max_steps=max_steps)
-    b = VecDroneEnv(n, device=dev, config=c, precision=precision, reward_mode="notebook", max_steps=max_steps)
+    a = VecDroneEnv(n, device=dev, config=c, precision=precision, reward_mode=mode, max_steps=max_steps)
+    b = VecDroneEnv(n, device=dev, config=c, precision=precision, reward_mode=mode, max_steps=max_steps)
     a.reset()
     b.reset()
     return a, b
@@ -38,15 +38,18 @@ def notebook_twins(n, dev, precision, max_steps, **cfg):
 def assert_same_env(a, b):
     for f in gd.FLOAT_FIELDS + ("status", "steps", "episode"):
         assert bits_equal(getattr(a, f), getattr(b, f)), f
-    assert bits_equal(a.shaped_hist, b.shaped_hist)
+    if a.shaped_hist is not None:  # PPO's history (REINFORCE's reward has none)
+        assert bits_equal(a.shaped_hist, b.shaped_hist)
 
 
+@pytest.mark.parametrize("mode", ["notebook", "reinforce"])
 @pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("auto_reset", [True, False])
 @pytest.mark.parametrize("n", [1037, 4100])
-def test_notebook_rollout_equals_step_loop(precision, auto_reset, n, gpu_device):
+def test_notebook_rollout_equals_step_loop(mode, precision, auto_reset, n, gpu_device):
     k, pre = 90, 3
-    roll, loop = notebook_twins(n, gpu_device, precision, 40, randomize_drone=True, auto_reset=auto_reset, seed=5)
+    roll, loop = notebook_twins(n, gpu_device, precision, 40, mode, randomize_drone=True, auto_reset=auto_reset,
+                                seed=5)
     g = torch.Generator(device=gpu_device).manual_seed(7)
     acts = torch.randint(0, 8, (pre + k + 1, n), device=gpu_device, generator=g, dtype=torch.uint8)
     for t in range(pre):  # start mid-episode: the history ring holds real distances
@@ -74,9 +77,10 @@ def test_notebook_rollout_equals_step_loop(precision, auto_reset, n, gpu_device)
     assert bits_equal(o1, o2) and bits_equal(r1, r2) and torch.equal(d1, d2)
 
 
-def test_notebook_rollout_philox_and_no_obs(gpu_device):
+@pytest.mark.parametrize("mode", ["notebook", "reinforce"])
+def test_notebook_rollout_philox_and_no_obs(mode, gpu_device):
     n, k = 2050, 70
-    roll, loop = notebook_twins(n, gpu_device, "f32", 25, randomize_drone=True, auto_reset=True, seed=8)
+    roll, loop = notebook_twins(n, gpu_device, "f32", 25, mode, randomize_drone=True, auto_reset=True, seed=8)
     _, reward, done = roll.rollout(frames=k, write_obs=False, action_seed=11)
     # the same in-kernel actions, one frame per launch
     r_all, d_all = [], []

@@ -496,6 +496,53 @@ def test_notebook_mode_matches_oracle_over_episodes(gpu_device):
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_reinforce_reward_vs_reference(precision, gpu_device):
+    """REINFORCE's calc_reward (Policy_Gradients.ipynb:162-238) + collect_episodes'
+    timeout (:590-593), fused into the step, against the notebook's own
+    outputs (tests/golden/reinforce_reward.npz).  Tolerance as the PPO reward's:
+    the kernel squares with x*x and takes the device's exp, the notebook glibc's
+    pow and exp, so terms may differ by an ulp."""
+    rec = gd.npz("reinforce_reward.npz")
+    n = rec["in_x"].shape[0]
+    env = VecDroneEnv(n, precision=precision, device=gpu_device, reward_mode="reinforce",
+                      max_steps=int(rec["max_steps"]))
+    load(env, gd.state_from_inputs(rec))
+    obs, shaped, sdone, info = env.step(torch.as_tensor(rec["in_action"], device=gpu_device))
+    np.testing.assert_array_equal(host(sdone), rec["out_shaped_done"])
+    want = rec["out_shaped"]
+    got = host(shaped).astype(np.float64)
+    if precision == "f64":
+        ok = f64_close(got, want, 8, 1e-9)
+    else:
+        ok = gd.f32_close(got, want, 2.0, 1e-6)
+    assert ok.all(), np.flatnonzero(~ok)[:5]
+    e_env, _, e_reward, e_done, _ = step_fixture(rec, precision, gpu_device)
+    assert np.array_equal(host(info["engine_reward"]), e_reward)
+
+
+def test_reinforce_mode_matches_oracle_over_episodes(gpu_device):
+    """Multi-frame REINFORCE mode: auto-reset, the 300-step timeout, against the
+    oracle's restatement of the notebook cell."""
+    n, frames = 4099, 700
+    cfg = EnvConfig(randomize_drone=True, auto_reset=True, seed=13)
+    env = VecDroneEnv(n, device=gpu_device, config=cfg, precision="f64", reward_mode="reinforce", max_steps=300)
+    env.reset()
+    o = ora.OracleEnv(n, precision="f64", config=cfg)
+    o.reset()
+    rng = np.random.default_rng(4)
+    worst, timeouts, landings = 0.0, 0, 0
+    for t in range(frames):
+        a = rng.integers(0, 8, n).astype(np.uint8)
+        _, shaped, sdone, _ = env.step(torch.as_tensor(a, device=gpu_device))
+        *_, oshaped, osdone = o.step_shaped(a, None, 300, mode="reinforce")
+        np.testing.assert_array_equal(host(sdone), osdone)
+        worst = max(worst, float(np.max(np.abs(host(shaped) - oshaped))))
+        timeouts += int(((host(env.steps) == 300) & host(sdone)).sum())
+    assert worst < 1e-9
+    assert timeouts > 0
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("auto", [True, False])
 def test_ping_pong_equals_in_place(precision, auto, gpu_device):
     """VecDroneEnv(ping_pong=True) (DDStepIO.state_out: read one copy of the

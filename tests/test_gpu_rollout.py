@@ -5,7 +5,7 @@ import pytest
 import torch
 
 import golden_data as gd
-from delivery_drone_amd import EnvConfig, VecDroneEnv
+from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
 from oracle import oracle as ora
 
 pytestmark = pytest.mark.gpu
@@ -225,10 +225,12 @@ def test_split_rollout_full_chip_equals_step_loop(precision, auto, gpu_device):
     assert_same_state(roll, loop)
     acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
     obs, reward, done = roll.rollout(acts)
+    assert roll.last_rollout_kernel == "split"
     for t in range(k):
         o, r, d, _ = loop.step(acts[t])
         assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
     assert_same_state(roll, loop)
+    roll.check_device_errors()  # no hand-over wait ran out
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
@@ -272,7 +274,8 @@ def test_rollout_short_episodes_equal_step_loop(precision, n, gpu_device):
     thrusting frames), so lanes end several episodes between two refills of
     the rollout's drawn-ahead re-spawn blocks (frame.h SpawnAhead, every 32nd
     frame): both the drawn-ahead and the in-frame draw, bit for bit the step
-    loop's; 65,532 lanes take the split kernel when the config allows it."""
+    loop's.  max_fuel 1.5 is not config.py's physics, so this is the single-role
+    kernel at both sizes; the split kernel's twin is the next test."""
     k = 37
     roll, loop = twins(n, gpu_device, precision, randomize_drone=True, randomize_platform=True, auto_reset=True,
                        seed=23, max_fuel=1.5)
@@ -283,6 +286,91 @@ def test_rollout_short_episodes_equal_step_loop(precision, n, gpu_device):
         assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
     assert_same_state(roll, loop)
     assert int(roll.episode.max()) >= 8  # several episodes between two refills on some lanes
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_split_rollout_reference_short_episodes_equal_step_loop(precision, gpu_device):
+    """The split kernel (config.py's physics) with lanes that end two episodes
+    inside one 32-frame refill interval, so its in-frame re-spawn draw runs
+    next to the drawn-ahead one: every lane starts just below the top edge
+    climbing (out of bounds on frame 0), and with the main engine on at angle 0
+    a re-spawn at y <= ~65 leaves through the top again within ~28 frames."""
+    n, k = 65_532, 64
+    roll, loop = twins(n, gpu_device, precision, randomize_drone=True, auto_reset=True, seed=41)
+    for env in (roll, loop):
+        env.y.fill_(-48.0)
+        env.vy.fill_(-5.0)
+    acts = torch.ones((k, n), device=gpu_device, dtype=torch.uint8)  # main engine only
+    obs, reward, done = roll.rollout(acts)
+    assert roll.last_rollout_kernel == "split"
+    ends_before_refill = done[:31].sum(dim=0)
+    for t in range(k):
+        o, r, d, _ = loop.step(acts[t])
+        assert torch.equal(obs[t], o) and torch.equal(reward[t], r) and torch.equal(done[t], d), t
+    assert_same_state(roll, loop)
+    assert int((ends_before_refill >= 2).sum()) > 100  # two episodes ended before frame 31 on these lanes
+    roll.check_device_errors()
+
+
+def test_split_rollout_handover_timeout_is_reported(gpu_device):
+    """a split-rollout hand-over wait that runs out is not silent.
+    kernel="no_wait" caps the waits at zero polls (the frame and writer waves
+    then race ahead of each other); dd_device_errors reports DD_ERR_HANDOVER,
+    the normal launch does not, and the bits clear once read."""
+    n = 65_532
+    env = VecDroneEnv(n, device=gpu_device, config=EnvConfig(randomize_drone=True, auto_reset=True, seed=3))
+    env.reset()
+    env.check_device_errors()
+    acts = torch.randint(0, 8, (64, n), device=gpu_device, dtype=torch.uint8)
+    env.rollout(acts)
+    assert env.last_rollout_kernel == "split"
+    env.check_device_errors()
+    env.rollout(acts, kernel="no_wait")
+    assert env.last_rollout_kernel == "split"
+    with pytest.raises(abi.NativeLibraryError, match="DD_ERR_HANDOVER"):
+        env.check_device_errors()
+    env.check_device_errors()  # read and cleared
+
+
+def test_rollout_kernel_single_equals_split(gpu_device):
+    """kernel="single" keeps the single-role kernel where the split one
+    applies; both equal the same frames bit for bit."""
+    n, k = 65_532, 40
+    a, b = twins(n, gpu_device, "f32", randomize_drone=True, auto_reset=True, seed=17)
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8)
+    oa, ra, da = a.rollout(acts)
+    assert a.last_rollout_kernel == "split"
+    ob, rb, db = b.rollout(acts, kernel="single")
+    assert b.last_rollout_kernel == "held"
+    assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
+    assert_same_state(a, b)
+
+
+def test_rollout_launch_groups_past_4gib_of_actions(gpu_device):
+    """dd_rollout reads actions by raw buffer loads with 32-bit
+    offsets, so rollout_chunks splits a rollout whose action rows span more than
+    4 GiB into several launches, passing the state through memory.  f32x3
+    actions at 2^22 + 37 lanes (50.3 MB per frame) over 90 frames make two
+    launches (85 + 5 frames); the result equals the same frames as 10-frame
+    rollouts (each under 4 GiB) bit for bit, the ragged tail included."""
+    n, k = (1 << 22) + 37, 90
+    roll, loop = twins(n, gpu_device, "f32", randomize_drone=True, auto_reset=True, seed=19)
+    g = torch.Generator(device=gpu_device).manual_seed(5)
+    bits = torch.randint(0, 8, (k, n), device=gpu_device, generator=g, dtype=torch.uint8)
+    acts = torch.empty(k, n, 3, device=gpu_device)
+    for j in range(3):
+        acts[:, :, j] = ((bits >> j) & 1).float()
+    del bits
+    assert (k - 1) * n * 12 + n * 12 > 2**32  # the action rows span more than 4 GiB
+    _, reward, done = roll.rollout(acts, write_obs=False)
+    parts_r, parts_d = [], []
+    for g0 in range(0, k, 10):
+        _, r, d = loop.rollout(acts[g0:g0 + 10], write_obs=False)
+        parts_r.append(r)
+        parts_d.append(d)
+    assert torch.equal(reward, torch.cat(parts_r)) and torch.equal(done, torch.cat(parts_d))
+    assert_same_state(roll, loop)
+    assert int(roll.episode.max()) > 1
 
 
 def test_step_out_buffers_equal_rollout(gpu_device):

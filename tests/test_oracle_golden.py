@@ -274,6 +274,20 @@ def test_oracle_notebook_reward_bit_exact():
     np.testing.assert_array_equal(hist[slot, np.arange(len(slot))], obs64[:, 9])
 
 
+def test_oracle_reinforce_reward_bit_exact():
+    """The REINFORCE notebook's calc_reward (Policy_Gradients.ipynb:162-238)
+    + collect_episodes' timeout (:590-593), against the notebook's own cell."""
+    rec = gd.npz("reinforce_reward.npz")
+    n = rec["in_x"].shape[0]
+    env = ora.OracleEnv(n, precision="f64")
+    env.load_state_dict(gd.state_from_inputs(rec))
+    *_, shaped, sdone = env.step_shaped(rec["in_action"], None, int(rec["max_steps"]), mode="reinforce")
+    np.testing.assert_array_equal(shaped, rec["out_shaped"])
+    np.testing.assert_array_equal(sdone, rec["out_shaped_done"])
+    assert (rec["out_shaped"] < -400).any() and rec["out_shaped_done"].any()  # timeouts and terminals covered
+    assert (rec["out_total"] > 400).any()  # landings: 500 + fuel * 100
+
+
 def test_oracle_notebook_reward_kat():
     k = gd.js("kat_notebooks.json")["actor_critic_ppo"]
     env = ora.OracleEnv(1, precision="f64")

@@ -106,3 +106,30 @@ def test_two_rank_gloo_matches_single_batch(tmp_path):
         np.testing.assert_array_equal(g[f], getattr(env, f), err_msg=f)
     assert float(g["wall"]) > 0
     assert env.episode.max() > 1  # episodes ended and re-spawned inside the window
+
+
+def _edge_main(rank, world, port, outdir):
+    """gather_state with an empty shard (total < world) and each rank passing
+    its fields in a different dict order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    total = 2
+    start, count = shard_bounds(total, rank, world)
+    ids = torch.arange(start, start + count)
+    fields = {"a": ids.to(torch.float32), "b": torch.stack([ids, -ids], 1).to(torch.float32),
+              "c": ids.to(torch.int32)}
+    if rank % 2:  # another insertion order on the odd ranks
+        fields = dict(reversed(list(fields.items())))
+    state = gather_state(fields, total, dst=0)
+    if rank == 0:
+        np.savez(os.path.join(outdir, "edge.npz"), **{k: v.numpy() for k, v in state.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_state_empty_shard_and_field_order(tmp_path):
+    tmp.spawn(_edge_main, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
+    g = np.load(tmp_path / "edge.npz")
+    np.testing.assert_array_equal(g["a"], [0.0, 1.0])
+    np.testing.assert_array_equal(g["b"], [[0.0, 0.0], [1.0, -1.0]])
+    np.testing.assert_array_equal(g["c"], [0, 1])

@@ -76,3 +76,17 @@ def test_no_bit_cast_of_vector_elements(path):
     with open(path) as f:
         bad = find_element_bit_casts(f.read())
     assert not bad, f"{os.path.basename(path)}: __builtin_bit_cast of a vector element (miscompiled): {bad}"
+
+
+PRODUCT = os.path.join(REPO, "reinforcement-learning-101_amd", "csrc")
+
+
+@pytest.mark.parametrize("path", [p for p in _device_files() if p.startswith(PRODUCT)], ids=os.path.basename)
+def test_product_sources_carry_no_lab_switches(path):
+    """lab code stays out of the product kernels.  Experiments are
+    A/B builds of committed revisions (tools/build_rev.sh), not -D switches or
+    environment reads compiled into the product sources."""
+    with open(path) as f:
+        text = f.read()
+    assert not re.search(r"\bDD_EXP_\w*", text), "lab switch DD_EXP_* in a product source"
+    assert "getenv" not in text, "environment-driven kernel choice in a product source"

@@ -17,8 +17,9 @@
 #   lab        tools/kernel_lab.py (VARIANTS, ENVS, LABARGS)
 #   roll       tools/rollout_lab.py (VARIANTS, ENVS, ROLLARGS e.g. --philox), appended to <tag>/roll.jsonl
 #   sqroll     SQ counters of dd_rollout per lab variant (tools/pmc_rollout_ab.sh; ROLLARGS, ROLLSUFFIX)
-#   roll5      config 5 only: rocprof kernel trace of 20 dd_rollout launches (65,536 x 256) and the
+#   roll5      config 5 only: rocprof kernel trace of bench.py's 161 dd_rollout launches (65,536 x 256) and the
 #              rollout kernel's FETCH_SIZE / WRITE_SIZE passes (tools/prof_driver.py --what rollout)
+#   c5clk      config 5: GRBM_GUI_ACTIVE / SQ cycles per dispatch (the DVFS clock of each launch)
 #   mr         tools/multirank_check.py on 2 gloo ranks sharing GPU 0 (torchrun), output in <tag>/mr/
 #   py:<file>  python <file> (LABARGS passed through), output in <tag>/<file stem>.log
 set -o pipefail
@@ -63,13 +64,23 @@ run_step() {
     sq)
         bash tools/pmc_sq.sh $OUT ;;
     roll5)
+        # bench.py's rollout_point schedule: 1 + 120 warm launches, then the 40 it times (last 40 of 161)
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_c5 -o roll -f csv -- python3 tools/prof_driver.py \
-            --what rollout --envs 65536 --frames 256 --reps 20 > /dev/null 2> $OUT/roll5.err || return 1
+            --what rollout --envs 65536 --frames 256 --reps 161 > /dev/null 2> $OUT/roll5.err || return 1
+        python3 tools/trace_summary.py $OUT/prof_c5/roll_kernel_trace.csv --kernel rollout_kernel --last 40 \
+            > $OUT/c5_trace_summary.json || return 1
         for C in FETCH_SIZE WRITE_SIZE; do
             timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex rollout_kernel -d $OUT/pmc_roll_$C -o pmc -f csv \
                 -- python3 tools/prof_driver.py --what rollout --envs 65536 --frames 256 --reps 5 > /dev/null \
                 2>> $OUT/roll5.err || return 1
         done ;;
+    c5clk)
+        # the effective shader clock per config-5 launch: GRBM_GUI_ACTIVE / 8 / duration (MI355X_MICROARCH, DVFS)
+        timeout -s KILL 150 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace \
+            -d $OUT/c5clk -o roll -f csv -- python3 tools/prof_driver.py --what rollout --envs 65536 --frames 256 \
+            --reps 161 > /dev/null 2> $OUT/c5clk.err || return 1
+        python3 tools/trace_summary.py $OUT/c5clk/roll_counter_collection.csv --kernel rollout_kernel --last 40 \
+            > $OUT/c5clk_summary.json ;;
     lab)
         timeout -k 10 600 python tools/kernel_lab.py --variants ${VARIANTS:-base} --envs ${ENVS:-262144,1048576,16777216} \
             ${LABARGS} > $OUT/lab.jsonl 2> $OUT/lab.err; local rc=$?; cat $OUT/lab.jsonl; tail -5 $OUT/lab.err; return $rc ;;

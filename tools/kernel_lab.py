@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """A/B timing of step-kernel builds, interleaved in one process.
 
-Each variant is a build of the same source with one -D switch
-(tools/build_variants.sh).  For every batch size, every variant gets its own
+Each variant is a library under _native/lab/: lib_base.so (a copy of the
+working tree's build) or a committed revision built by tools/build_rev.sh.  For every batch size, every variant gets its own
 VecDroneEnv (config-3 workload: random spawn, auto-reset, obs on), a captured
 hipGraph of G steps, and R interleaved rounds of replays timed with HIP events
 on the replay stream.  Prints one JSON line per (N, variant): median and min
@@ -34,6 +34,9 @@ def main():
     p.add_argument("--rounds", type=int, default=9)
     p.add_argument("--precision", default="f32")
     p.add_argument("--no-obs", action="store_true")
+    p.add_argument("--allocs", type=int, default=1,
+                   help="identical envs allocated one after another; every variant steps each of them "
+                        "(the HBM point's placement spread, DESIGN.md §4, then shows per allocation)")
     p.add_argument("--separate", dest="shared", action="store_false",
                    help="one env per variant (default: every variant steps the same buffers)")
     args = p.parse_args()
@@ -45,30 +48,33 @@ def main():
         rows = torch.randint(0, 8, (8, n), device=dev, dtype=torch.uint8)
         stream = torch.cuda.Stream(dev)
         runs = {}
-        shared = None
-        for name, lib in libs.items():
-            if shared is None or not args.shared:
-                env = VecDroneEnv(n, device=dev, config=cfg, precision=args.precision, library=lib)
-                env.reset()
-                shared = env
-            else:  # the same buffers, another build: physical placement out of the A/B
-                env = shared
-            env._lib = lib
-            with torch.cuda.stream(stream):
-                for k in range(3):
-                    env.step(rows[k], write_obs=not args.no_obs)
+        allocs = []
+        for a in range(max(1, args.allocs)):
+            shared = None
+            for name, lib in libs.items():
+                if shared is None or not args.shared:
+                    env = VecDroneEnv(n, device=dev, config=cfg, precision=args.precision, library=lib)
+                    env.reset()
+                    shared = env
+                    allocs.append(env)
+                else:  # the same buffers, another build: physical placement out of the A/B
+                    env = shared
+                env._lib = lib
+                with torch.cuda.stream(stream):
+                    for k in range(3):
+                        env.step(rows[k], write_obs=not args.no_obs)
+                    torch.cuda.synchronize(dev)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=stream):
+                        for k in range(G):
+                            env.step(rows[k % 8], write_obs=not args.no_obs)
+                    g.replay()
                 torch.cuda.synchronize(dev)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=stream):
-                    for k in range(G):
-                        env.step(rows[k % 8], write_obs=not args.no_obs)
-                g.replay()
-            torch.cuda.synchronize(dev)
-            runs[name] = (env, g, [])
-        names = list(runs)
+                runs[(name, a)] = (env, g, [])
+        keys = list(runs)
         for rnd in range(args.rounds):  # ABBA: alternate the order so position effects cancel
-            for name in (names if rnd % 2 == 0 else names[::-1]):
-                env, g, times = runs[name]
+            for key in (keys if rnd % 2 == 0 else keys[::-1]):
+                env, g, times = runs[key]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 with torch.cuda.stream(stream):
                     e0.record(stream)
@@ -76,14 +82,17 @@ def main():
                     e1.record(stream)
                 torch.cuda.synchronize(dev)
                 times.append(e0.elapsed_time(e1) * 1e3 / G)
-        for name, (env, g, times) in runs.items():
+        for (name, a), (env, g, times) in runs.items():
             med = statistics.median(times)
             bpe = env.step_bytes_per_env(with_obs=not args.no_obs)
-            print(json.dumps({"envs": n, "variant": name, "us_per_step_median": round(med, 3),
-                              "us_per_step_min": round(min(times), 3),
-                              "gbs_median": round(bpe * n / (med * 1e-6) / 1e9, 1),
-                              "steps_per_s": round(n / (med * 1e-6), 1)}), flush=True)
-        del runs
+            row = {"envs": n, "variant": name, "us_per_step_median": round(med, 3),
+                   "us_per_step_min": round(min(times), 3),
+                   "gbs_median": round(bpe * n / (med * 1e-6) / 1e9, 1),
+                   "steps_per_s": round(n / (med * 1e-6), 1)}
+            if args.allocs > 1:
+                row["allocation"] = a
+            print(json.dumps(row), flush=True)
+        del runs, allocs
         torch.cuda.empty_cache()
 
 

@@ -1,0 +1,45 @@
+#!/usr/bin/env python
+"""Per-launch durations of one kernel from a rocprofv3 kernel trace (and, for
+a counter-collection CSV, the effective clock GRBM_GUI_ACTIVE / 8 / duration
+per dispatch), with the averages over all launches and over the last N — the
+launches bench.py times after its warm ones (rollout_point: 1 + 120 warm, 40
+timed).
+
+    python tools/trace_summary.py TRACE.csv --kernel rollout_kernel --last 40
+"""
+import argparse
+import csv
+import json
+import re
+import statistics
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("csv")
+    p.add_argument("--kernel", default="rollout_kernel")
+    p.add_argument("--last", type=int, default=40)
+    args = p.parse_args()
+    rows = [r for r in csv.DictReader(open(args.csv)) if re.search(args.kernel, r["Kernel_Name"])]
+    per = {}
+    for r in rows:
+        d = per.setdefault(int(r["Dispatch_Id"]), {"us": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3,
+                                                   "kernel": r["Kernel_Name"]})
+        if "Counter_Name" in r:
+            d[r["Counter_Name"]] = float(r["Counter_Value"])
+    ids = sorted(per)
+    us = [per[i]["us"] for i in ids]
+    out = {"source": args.csv, "kernel_regex": args.kernel, "kernels": sorted({per[i]["kernel"] for i in ids}),
+           "launches": len(us), "us_mean_all": round(statistics.mean(us), 2),
+           "last": args.last, "us_mean_last": round(statistics.mean(us[-args.last:]), 2),
+           "us_median_last": round(statistics.median(us[-args.last:]), 2),
+           "us_per_launch": [round(u, 1) for u in us]}
+    if ids and "GRBM_GUI_ACTIVE" in per[ids[0]]:
+        ghz = [per[i]["GRBM_GUI_ACTIVE"] / 8 / (per[i]["us"] * 1e3) for i in ids]
+        out["effective_clock_ghz"] = [round(g, 3) for g in ghz]
+        out["shader_kcycles_per_launch"] = [round(g * u, 1) for g, u in zip(ghz, us)]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
