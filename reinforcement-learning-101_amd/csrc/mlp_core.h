@@ -39,15 +39,17 @@ constexpr int kV2 = kV1 + 3 * 128;
 constexpr int kV3 = kV2 + 3 * 128;  // [3][64]
 constexpr int kW4 = kV3 + 3 * 64;   // last layer [3][64], rows >= K zero
 constexpr int kB4 = kW4 + 3 * 64;   // bias [3], LayerNorm eps
-constexpr int kTag = kB4 + 4;       // layout tag [4]: pack_tag(compute, K), then zeros
+constexpr int kTag = kB4 + 4;       // layout tag [4]: pack_tag(compute, K), then the three LayerNorms' eps
+constexpr int kEps = kTag + 1;      // eps of LayerNorm 1, 2, 3 (DD_MLP_F16X3: scaled, below)
 constexpr int kPacked = kTag + 4;
 constexpr size_t kLdsBytes = kPacked * sizeof(float);
 static_assert(kPacked % 4 == 0, "packed buffer is read as float4");
 
 // What dd_mlp_pack wrote the buffer for: the A sections' arithmetic
-// (DD_MLP_*) and the output width K, as the payload of a quiet NaN.
+// (DD_MLP_*) and the output width K, as the payload of a quiet NaN (0xDE:
+// the round-5 layout, scaled f16x3 sections and per-layer eps).
 __host__ __device__ constexpr uint32_t pack_tag(int compute, int out_dim) {
-    return 0x7FC0DD00u | ((uint32_t)compute << 4) | (uint32_t)out_dim;
+    return 0x7FC0DE00u | ((uint32_t)compute << 4) | (uint32_t)out_dim;
 }
 
 // Float4 i of the packed buffer on its way into LDS.  The fragment holding
@@ -75,31 +77,43 @@ constexpr bool kCentered = true;
 __host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // ---- DD_MLP_F16X3: split operands on the f16 MFMA --------------------------
+// Every operand is split a = hi + lo, hi = f16(a), lo = f16(a - hi), both
+// rounded to nearest-even (a - hi is exact in f32), and a product is
+// hi.hi + hi.lo + lo.hi + O(2^-22): three f16 MFMAs per k-step, each
+// product exact, all three accumulated into ONE f32 accumulator that starts
+// at the Linear's bias — no per-layer rescale pass (round 4's lo' = (a -
+// hi) 2^11 needed the cross terms in their own pass, scaled back by 2^-11
+// with one FMA per accumulator register: 160 VALU per tile).  lo stays clear
+// of the f16 subnormals by scaling the operands by powers of two, which every
+// LayerNorm removes exactly (LN(c x) = LN(x) with eps c^2):
+//   * hidden weights x kWScale, the layer-1 input x kInScale (in registers),
+//     each LayerNorm's output x kActScale (its weight and bias, packed);
+//   * each Linear's bias x kWScale x (its input's scale), each LayerNorm's
+//     eps x (that product)^2 (kEps), the last Linear's weights / kActScale.
+// Operand range: |weights| < 4094, |observations| < 1023, LayerNorm outputs
+// < 4094 (f16's 65504).  Notebook models: actor probabilities within 4.4e-7
+// of float64, critic values within 2.4e-4 (the former scheme 5.6e-7 /
+// 2.1e-4; tools/mlp_split_sim.py --single-acc).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr float kLoScale = 2048.0f;  // 2^11: lo' lives at hi's magnitude (no f16 subnormals)
-constexpr float kLoUnscale = 1.0f / 2048.0f;
+constexpr float kWScale = 16.0f;    // 2^4
+constexpr float kInScale = 64.0f;   // 2^6
+constexpr float kActScale = 16.0f;  // 2^4
 
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-// Two floats -> packed f16 hi and lo' halves, each rounded to nearest-even
-// (v_cvt_pk_f16_f32).  a - hi is exact in f32 (hi is a to 11 bits), the
-// scaling by 2^11 too.  (Truncating instead, v_cvt_pkrtz, biases lo' and
-// quadruples the end-to-end error: tools/mlp_split_sim.py --truncate.)
-// The residual (a - hi) 2^11 is one v_fma_mix_f32 per element,
-// fma(-hi, 2^11, a 2^11) with hi read as f16 straight from the packed
-// register (exact: the product and the sum are exact, so the one rounding
-// changes nothing): v_cvt_pk_f16_f32, v_pk_mul_f32, two v_fma_mix_f32,
-// v_cvt_pk_f16_f32 = 5 VALU per pair, the same bits as converting hi back to
-// f32 and subtracting (6; tools/mlp_equal_check.py).
+// Two floats -> packed f16 hi and lo halves, each rounded to nearest-even
+// (v_cvt_pk_f16_f32).  (Truncating instead, v_cvt_pkrtz, biases lo and
+// quadruples the end-to-end error: tools/mlp_split_sim.py --truncate.)  The
+// residual a - hi is one v_fma_mix_f32 per element, fma(-hi, 1, a) with hi
+// read as f16 straight from the packed register (exact): v_cvt_pk_f16_f32,
+// two v_fma_mix_f32, v_cvt_pk_f16_f32 = 4 VALU per pair.
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
     uint32_t hp = __builtin_bit_cast(uint32_t, f16x2{(_Float16)a, (_Float16)b});
     asm("" : "+v"(hp));  // widen hi from the packed register (else each half is converted twice)
-    const f32x2 as = f32x2{a, b} * f32x2{kLoScale, kLoScale};
     f32x2 r;
-    asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r.x) : "v"(hp), "v"(kLoScale), "v"(as.x));
-    asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r.y) : "v"(hp), "v"(kLoScale),
-        "v"(as.y));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r.x) : "v"(hp), "v"(a));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r.y) : "v"(hp), "v"(b));
     const f16x2 l = {(_Float16)r.x, (_Float16)r.y};
     hi = hp;
     lo = __builtin_bit_cast(uint32_t, l);
@@ -144,42 +158,59 @@ __device__ __forceinline__ void layer_mfma(const f32x4* __restrict__ a4, int lan
     }
 }
 
-// out^T tiles (NT of 32 rows) = bias + W . in^T over KS k-steps of 16.  The
-// packed A fragments are [tile][k-step][hi | lo'][lane] x 16 B; bh / bl are
-// the lane's B fragments.  The cross terms go first into the zeroed
-// accumulator, which is then scaled by 2^-11 and given the bias, and the
-// hi.hi products accumulate on top: one accumulator per tile.
-template <int NT, int KS>
-__device__ __forceinline__ void layer16(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
-                                        const f16x8 (&bl)[KS], f32x16 (&acc)[NT], const float* bias_h) {
+// The bias as an accumulator's initial value (the lane half's rows).
+template <int NT>
+__device__ __forceinline__ void bias_init(f32x16 (&acc)[NT], const float* bias_h) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
+        for (int r = 0; r < 16; ++r) acc[t][r] = bias_h[hid(t, r, 0)];
+}
+
+// The three f16 MFMAs of one k-step into NT out tiles' accumulators: the two
+// small cross terms, then hi.hi.  kWide: each term over the tiles in turn, so
+// that consecutive MFMAs write different accumulators (NT hi fragments live);
+// otherwise tile by tile (the fused policy rollout, at its register cap).
+// blk(t): tile t's k-step fragment block [hi | lo][lane] (each A fragment
+// read once).
+template <int NT, bool kWide, typename Blk>
+__device__ __forceinline__ void mfma3(Blk blk, int lane, const f16x8& bh, const f16x8& bl, f32x16 (&acc)[NT]) {
+    if constexpr (!kWide) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            const u32x4* blk = a16 + (t * KS + s) * 128;
-            const f16x8 ah = __builtin_bit_cast(f16x8, blk[lane]);
-            const f16x8 al = __builtin_bit_cast(f16x8, blk[64 + lane]);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc[t], 0, 0, 0);
+            const f16x8 ah = __builtin_bit_cast(f16x8, blk(t)[lane]);
+            const f16x8 al = __builtin_bit_cast(f16x8, blk(t)[64 + lane]);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[t], 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);  // keep each k-step's LDS reads next to its MFMAs
+        return;
+    }
+    f16x8 ah[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        ah[t] = __builtin_bit_cast(f16x8, blk(t)[lane]);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bl, acc[t], 0, 0, 0);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, blk(t)[64 + lane]), bh, acc[t], 0,
+                                                        0, 0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
+    for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bh, acc[t], 0, 0, 0);
+}
+
+// out^T tiles (NT of 32 rows) = bias + W . in^T over KS k-steps of 16.  The
+// packed A fragments are [tile][k-step][hi | lo][lane] x 16 B (each A
+// fragment read once); bh / bl are the lane's B fragments.
+template <int NT, int KS, bool kWide>
+__device__ __forceinline__ void layer16(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
+                                        const f16x8 (&bl)[KS], f32x16 (&acc)[NT], const float* bias_h) {
+    bias_init<NT>(acc, bias_h);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const f16x8 ah = __builtin_bit_cast(f16x8, a16[(t * KS + s) * 128 + lane]);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[t], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+        mfma3<NT, kWide>([&](int t) { return a16 + (t * KS + s) * 128; }, lane, bh[s], bl[s], acc);
+        __builtin_amdgcn_sched_barrier(0);  // keep each k-step's LDS reads next to its MFMAs
     }
 }
 
@@ -270,58 +301,27 @@ struct NoMid {
     __device__ void operator()() const {}
 };
 
-// norm_relu_split of a 128-row layer fused with the next layer's cross terms
-// (layer16's first loop): as soon as hidden tile t is split, the MFMAs of
-// k-steps 2t and 2t + 1 (which read only its fragments) are issued, so the
-// split of tile t + 1 can run in their shadow (a wave's own VALU does overlap
-// its own MFMAs; another wave's does not: tools/micro/mfma_valu_overlap.hip).
-// Each accumulator sees the same MFMAs in the same order as layer16's, so the
-// result is bit-identical; layer16_hihi finishes the layer.
+// norm_relu_split of a 128-row layer fused with the next layer: as soon as
+// hidden tile t is split, the MFMAs of k-steps 2t and 2t + 1 (which read only
+// its fragments) are issued, so the split of tile t + 1 can run in their
+// shadow (a wave's own VALU does overlap its own MFMAs; another wave's does
+// not: tools/micro/mfma_valu_overlap.hip).  Each accumulator sees the same
+// MFMAs in the same order as layer16's, so the result is bit-identical.
 template <int NTO>
-__device__ __forceinline__ void norm_split_cross(const f32x16 (&acc)[4], const float* vec, float eps, int h,
-                                                 const u32x4* __restrict__ a16n, int lane, f16x8 (&bh)[8],
-                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO]) {
-#pragma unroll
-    for (int to = 0; to < NTO; ++to)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) out[to][r] = 0.0f;
+__device__ __forceinline__ void norm_split_next(const f32x16 (&acc)[4], const float* vec, float eps, int h,
+                                                const u32x4* __restrict__ a16n, int lane, f16x8 (&bh)[8],
+                                                f16x8 (&bl)[8], f32x16 (&out)[NTO], const float* bias_n) {
+    bias_init<NTO>(out, bias_n);
     auto emit = [&](int t, const float (&v)[16]) {
         split8(&v[0], bh[2 * t], bl[2 * t]);
         split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int s = 2 * t + q;
-#pragma unroll
-            for (int to = 0; to < NTO; ++to) {
-                const u32x4* blk = a16n + (to * 8 + s) * 128;
-                const f16x8 ah = __builtin_bit_cast(f16x8, blk[lane]);
-                const f16x8 al = __builtin_bit_cast(f16x8, blk[64 + lane]);
-                out[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], out[to], 0, 0, 0);
-                out[to] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], out[to], 0, 0, 0);
-            }
+            mfma3<NTO, true>([&](int to) { return a16n + (to * 8 + s) * 128; }, lane, bh[s], bl[s], out);
         }
     };
     norm_relu_emit<4, decltype(emit), false>(acc, vec, eps, h, emit);
-}
-
-// The rest of layer16 after its cross terms: scale them by 2^-11, add the
-// bias, accumulate the hi.hi products.
-template <int NT, int KS>
-__device__ __forceinline__ void layer16_hihi(const u32x4* __restrict__ a16, int lane, const f16x8 (&bh)[KS],
-                                             f32x16 (&acc)[NT], const float* bias_h) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = fmaf(acc[t][r], kLoUnscale, bias_h[hid(t, r, 0)]);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const f16x8 ah = __builtin_bit_cast(f16x8, a16[(t * KS + s) * 128 + lane]);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[t], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
 }
 
 // log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
@@ -361,45 +361,47 @@ __device__ __forceinline__ void head_of(const float* lds, int h, const float (&y
 // (kSplit, one k-step of 16), zero past column 14.  Every lane ends with z
 // of its column.  lds: the packed parameters.  mid() runs between layer 1
 // and layer 2 (dd_mlp_forward waits there for layers 2-3 of its LDS image).
-// kPipe: layer 2's split runs in the shadow of layer 3's cross-term MFMAs
-// (norm_split_cross, +16 VGPRs); the fused policy rollout, at the register
-// cap, takes the serial schedule.  Both give the same bits.
+// kPipe: layer 2's split runs in the shadow of layer 3's MFMAs
+// (norm_split_next); the fused policy rollout, at the register cap, takes
+// the serial schedule.  Both give the same bits.
 template <int K, bool kSplit, bool kPipe = true, typename Mid = NoMid>
 __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float (&x)[8], float (&z)[K],
                                          Mid mid = {}) {
     const f32x4* lds4 = reinterpret_cast<const f32x4*>(lds);
     const int h = lane >> 5;
-    const float eps = lds[kB4 + 3];
+    const float eps1 = lds[kEps], eps2 = lds[kEps + 1], eps3 = lds[kEps + 2];
     f32x16 acc4[4];
     f32x16 acc2[2];
     float y3[2][16];
     if constexpr (kSplit) {
         const u32x4* a16 = reinterpret_cast<const u32x4*>(lds);
         f16x8 b1h[1], b1l[1], bh[8], bl[8];
-        split8(x, b1h[0], b1l[0]);
-        layer16<4, 1>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
-        norm_relu_split<4>(acc4, lds + kV1, eps, h, bh, bl);
+        float xs[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xs[q] = x[q] * kInScale;  // exact: a power of two
+        split8(xs, b1h[0], b1l[0]);
+        layer16<4, 1, kPipe>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
+        norm_relu_split<4>(acc4, lds + kV1, eps1, h, bh, bl);
         mid();
-        layer16<4, 8>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
+        layer16<4, 8, kPipe>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
         if constexpr (kPipe) {
-            norm_split_cross<2>(acc4, lds + kV2, eps, h, a16 + kA3 / 4, lane, bh, bl, acc2);
-            layer16_hihi<2, 8>(a16 + kA3 / 4, lane, bh, acc2, lds + kV3 + 4 * h);
+            norm_split_next<2>(acc4, lds + kV2, eps2, h, a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
         } else {  // layer 2's LayerNorm + split, then all of layer 3
-            norm_relu_split<4>(acc4, lds + kV2, eps, h, bh, bl);
-            layer16<2, 8>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+            norm_relu_split<4>(acc4, lds + kV2, eps2, h, bh, bl);
+            layer16<2, 8, kPipe>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
         }
-        norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        norm_relu<2>(acc2, lds + kV3, eps3, h, y3);
     } else {
         float y1[4][16], y2[4][16];
         layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
-        norm_relu<4>(acc4, lds + kV1, eps, h, y1);
+        norm_relu<4>(acc4, lds + kV1, eps1, h, y1);
         mid();
         layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4,
                                lds + kV2 + 4 * h);
-        norm_relu<4>(acc4, lds + kV2, eps, h, y2);
+        norm_relu<4>(acc4, lds + kV2, eps2, h, y2);
         layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2,
                                lds + kV3 + 4 * h);
-        norm_relu<2>(acc2, lds + kV3, eps, h, y3);
+        norm_relu<2>(acc2, lds + kV3, eps3, h, y3);
     }
     __builtin_amdgcn_sched_barrier(0);
     head_of<K>(lds, h, y3, z);

@@ -28,12 +28,13 @@
 //
 // DD_MLP_F16X3 (opt-in) runs the three hidden GEMMs on the f16 MFMA
 // (v_mfma_f32_32x32x16_f16, 16x the f32 MFMA's rate) with every operand
-// split in two halves, a = hi + lo' * 2^-11 (hi = f16(a), lo' = f16((a - hi)
-// * 2^11), both nearest-even): a . b = hi.hi + 2^-11 (hi.lo' + lo'.hi) + O(2^-22),
-// three f16 MFMAs per k-step of 16, products exact and summed in f32, so a
-// dot product carries about the f32 path's error (the notebook's actor
+// split in two halves, a = hi + lo (hi = f16(a), lo = f16(a - hi), both
+// nearest-even): a . b = hi.hi + hi.lo + lo.hi + O(2^-22), three f16 MFMAs
+// per k-step of 16 into one f32 accumulator, products exact, so a dot
+// product carries about the f32 path's error (the notebook's actor
 // probabilities within 5e-7 of float64 either way, tools/mlp_split_sim.py).
-// Operands must stay below 65504 in magnitude (f16 range).
+// The operands are scaled by powers of two that the LayerNorms remove
+// (mlp_core.h): |weights| < 4094, |observations| < 1023.
 
 #include <hip/hip_runtime.h>
 #include <float.h>
@@ -86,7 +87,7 @@ __device__ __forceinline__ float pack_a16(const DDMlpParams& p, int i) {
     for (int e = 0; e < 2; ++e) {
         const int j = 2 * m + e;
         const int col = base == kA1 ? 8 * h + j : hid(s >> 1, 8 * (s & 1) + j, h);
-        v[e] = weight_at(p, base, row, col);
+        v[e] = weight_at(p, base, row, col) * kWScale;  // exact: a power of two
     }
     uint32_t hi, lo;
     split_pair(v[0], v[1], hi, lo);
@@ -97,6 +98,7 @@ __device__ __forceinline__ float pack_a16(const DDMlpParams& p, int i) {
 __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= kPacked) return;
+    const bool split = compute == DD_MLP_F16X3;
     float v = 0.0f;
     if (i < kV1 && compute == DD_MLP_F16X3) {
         v = pack_a16(p, i);
@@ -111,26 +113,25 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
         // (t', r) = q takes hidden row hid(t', r, h)
         const int col = base == kA1 ? 2 * q + h : hid(q >> 4, q & 15, h);
         v = weight_at(p, base, row, col);
-    } else if (i < kV2) {
-        const int o = i - kV1;
-        const float* src[3] = {p.b0, p.ln1_w, p.ln1_b};
-        v = o < 128 ? bias_at(p.b0, 128, o) : src[o / 128][o % 128];
-    } else if (i < kV3) {
-        const int o = i - kV2;
-        const float* src[3] = {p.b3, p.ln4_w, p.ln4_b};
-        v = o < 128 ? bias_at(p.b3, 128, o) : src[o / 128][o % 128];
-    } else if (i < kW4) {
-        const int o = i - kV3;
-        const float* src[3] = {p.b6, p.ln7_w, p.ln7_b};
-        v = o < 64 ? bias_at(p.b6, 64, o) : src[o / 64][o % 64];
+    } else if (i < kW4) {  // [bias | LN weight | LN bias] of layers 1-3
+        const int L = i < kV2 ? 0 : i < kV3 ? 1 : 2, rows = L == 2 ? 64 : 128;
+        const int o = i - (L == 0 ? kV1 : L == 1 ? kV2 : kV3);
+        const float* src[3][3] = {{p.b0, p.ln1_w, p.ln1_b}, {p.b3, p.ln4_w, p.ln4_b}, {p.b6, p.ln7_w, p.ln7_b}};
+        v = o < rows ? bias_at(src[L][0], rows, o) : src[L][o / rows][o % rows];
+        if (split)  // the bias at its GEMM's scale (weights x input); the LN's affine at the next input's
+            v *= o < rows ? kWScale * (L == 0 ? kInScale : kActScale) : kActScale;
     } else if (i < kB4) {
         const int o = i - kW4;
         v = (o / 64) < p.out_dim ? p.w9[o] : 0.0f;
+        if (split) v *= 1.0f / kActScale;  // the last LayerNorm's output is kActScale x
     } else if (i < kTag) {
         const int o = i - kB4;
         v = o < p.out_dim ? p.b9[o] : (o == 3 ? p.ln_eps : 0.0f);
-    } else {
-        v = i == kTag ? __uint_as_float(pack_tag(compute, p.out_dim)) : 0.0f;
+    } else if (i == kTag) {
+        v = __uint_as_float(pack_tag(compute, p.out_dim));
+    } else {  // kEps: each LayerNorm's eps at its input's scale squared
+        const float sc = !split ? 1.0f : kWScale * (i == kEps ? kInScale : kActScale);
+        v = p.ln_eps * sc * sc;
     }
     out[i] = v;
 }

@@ -1,0 +1,63 @@
+#!/usr/bin/env python
+"""A lab build of the working tree with one source edit, for A/B runs
+(tools/kernel_lab.py, tools/lab/mlp_lab.py, tools/lab/prl_lab.py): copies
+reinforcement-learning-101_amd/csrc to /tmp, applies string replacements to
+one source (each OLD must occur exactly once), compiles that source and links
+it with the product's other objects into _native/lab/lib_NAME.so.  The
+product sources stay free of lab switches.
+
+    python tools/lab/build_variant.py NAME FILE OLD NEW [OLD NEW ...]
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+PKG = os.path.join(REPO, "reinforcement-learning-101_amd")
+FLAGS = {"policy_mlp": ["-mllvm", "-disable-machine-licm"], "policy_rollout": ["-mllvm", "-disable-machine-licm"]}
+
+
+def main():
+    name, fname, edits = sys.argv[1], sys.argv[2], sys.argv[3:]
+    src = f"/tmp/dd_variant_{name}"
+    shutil.rmtree(src, ignore_errors=True)
+    shutil.copytree(os.path.join(PKG, "csrc"), src)
+    path = os.path.join(src, fname)
+    text = open(path).read()
+    for old, new in zip(edits[::2], edits[1::2]):
+        if text.count(old) != 1:
+            raise SystemExit(f"{fname}: {old!r} occurs {text.count(old)} times")
+        text = text.replace(old, new)
+    open(path, "w").write(text)
+    # the translation units the edit lands in (a header: every unit that includes it)
+    def includes(f, seen=None):
+        seen = seen if seen is not None else set()
+        for line in open(os.path.join(src, f)):
+            if line.startswith('#include "'):
+                inc = line.split('"')[1]
+                if inc not in seen and os.path.exists(os.path.join(src, inc)):
+                    seen.add(inc)
+                    includes(inc, seen)
+        return seen
+    units = [u for u in ("drone_step", "policy_mlp", "policy_rollout", "render")
+             if fname == u + ".hip" or fname in includes(u + ".hip")]
+    objs = []
+    for u in ("drone_step", "policy_mlp", "policy_rollout", "render"):
+        if u in units:
+            o = os.path.join(src, u + ".o")
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                            "-fPIC", f"-I{os.path.join(REPO, 'include')}", f"-I{src}", *FLAGS.get(u, []),
+                            "-c", "-o", o, os.path.join(src, u + ".hip")], check=True)
+        else:
+            o = os.path.join(PKG, "build", "obj", u + ".o")
+        objs.append(o)
+    objs.append(os.path.join(PKG, "build", "obj", "build_info.o"))
+    out = os.path.join(PKG, "delivery_drone_amd", "_native", "lab", f"lib_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", out, *objs], check=True)
+    print(f"built {out} ({fname}: {len(edits) // 2} edit(s); rebuilt {units})")
+
+
+if __name__ == "__main__":
+    main()

@@ -46,15 +46,30 @@ def main():
             if err > 1e-5:
                 print(json.dumps({"variant": v, "rows": n, "MISMATCH": err}), flush=True)
         torch.cuda.synchronize()
+        # each variant's `reps` calls captured in a hipGraph: device time, not the
+        # host's launch rate (eager calls cost ~9 us each on the host)
+        stream = torch.cuda.Stream(dev)
+        graphs = {}
+        for v, (m, _) in nets.items():
+            with torch.cuda.stream(stream):
+                m.act(obs, actions_out=acts, log_prob_out=lp)
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=stream):
+                    for s in range(args.reps):
+                        m.act(obs, step=s, actions_out=acts, log_prob_out=lp)
+                g.replay()
+            graphs[v] = g
+        torch.cuda.synchronize()
         names = list(nets)
         for rnd in range(args.rounds):  # ABBA: alternate the order so position effects cancel
             for v in (names if rnd % 2 == 0 else names[::-1]):
                 m, ts = nets[v]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for s in range(args.reps):
-                    m.act(obs, step=s, actions_out=acts, log_prob_out=lp)
-                e1.record()
+                with torch.cuda.stream(stream):
+                    e0.record(stream)
+                    graphs[v].replay()
+                    e1.record(stream)
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e3 / args.reps)
         for v, (m, ts) in nets.items():

@@ -5,7 +5,11 @@ to plain float32.  Operands split as a = hi + lo * 2^-11 with hi, lo f16
 (both rounded to nearest-even: truncating them, v_cvt_pkrtz, biases lo and
 quadruples the error; run with --truncate), products exact, sums rounded to f32.
 --center: the hidden Linears mean-centred over their outputs and the LayerNorm
-without its mean pass, as dd_mlp_pack / norm_relu_emit do (mlp_core.h kCentered)."""
+without its mean pass, as dd_mlp_pack / norm_relu_emit do (mlp_core.h kCentered).
+The `single` rows emulate the round-5 form (mlp_core.h): lo = f16(a - hi)
+unscaled, the three products in one accumulator from the bias, hidden weights
+x16, the layer-1 input x64, LayerNorm outputs x16 (powers of two the
+LayerNorms remove), centred weights."""
 import sys
 
 import numpy as np
@@ -67,3 +71,42 @@ for pre in ('actor', 'critic'):
             print(pre, mode, 'max |dprob| vs f64', np.abs(p - pr).max(), 'vs golden', np.abs(p - d['probs']).max())
         else:
             print(pre, mode, 'max |dv| vs f64', np.abs(z[:,0]-ref[:,0]).max(), 'vs golden', np.abs(z[:,0]-d['values']).max(), 'max|v|', np.abs(ref).max())
+
+
+def split_unscaled(a):
+    a = a.astype(np.float32)
+    hi = a.astype(np.float16)
+    return hi, (a - hi.astype(np.float32)).astype(np.float16)  # lo may be an f16 subnormal
+
+
+def fwd_single(pre, w=4, am=4, im=6):
+    """The round-5 f16x3 form; the power-of-two scales of mlp_core.h (kWScale 2^w,
+    kInScale 2^im, kActScale 2^am)."""
+    f = lambda a: a.astype(np.float64)  # noqa: E731
+    x = d['obs'].astype(np.float32) * np.float32(2.0 ** im)
+    s_in = 2.0 ** im
+    for i, j in ((0, 1), (3, 4), (6, 7)):
+        W, b = d[f'{pre}.network.{i}.weight'], d[f'{pre}.network.{i}.bias']
+        W = (W.astype(np.float64) - W.astype(np.float64).mean(0, keepdims=True)).astype(np.float32)
+        b = (b.astype(np.float64) - b.astype(np.float64).mean()).astype(np.float32)
+        Wh, Wl = split_unscaled(W * np.float32(2.0 ** w))
+        xh, xl = split_unscaled(x)
+        sc = np.float32(2.0 ** w * s_in)
+        acc = (f(xh) @ f(Wh).T + f(xh) @ f(Wl).T + f(xl) @ f(Wh).T + f((b * sc).astype(np.float32))).astype(np.float32)
+        z = acc * (1 / np.sqrt((acc ** 2).mean(1, keepdims=True) + np.float32(1e-5) * sc * sc))
+        g = d[f'{pre}.network.{j}.weight'].astype(np.float32) * np.float32(2.0 ** am)
+        be = d[f'{pre}.network.{j}.bias'].astype(np.float32) * np.float32(2.0 ** am)
+        x = np.maximum(z * g + be, 0).astype(np.float32)
+        s_in = 2.0 ** am
+    W4 = d[f'{pre}.network.9.weight'].astype(np.float32) * np.float32(2.0 ** -am)
+    return (x @ W4.T + d[f'{pre}.network.9.bias']).astype(np.float32)
+
+
+for pre in ('actor', 'critic'):
+    ref = fwd(pre, 'f64')
+    z = fwd_single(pre)
+    if pre == 'actor':
+        p = 1 / (1 + np.exp(-z.astype(np.float64)))
+        print(pre, 'single', 'max |dprob| vs f64', np.abs(p - 1 / (1 + np.exp(-ref))).max())
+    else:
+        print(pre, 'single', 'max |dv| vs f64', np.abs(z[:, 0] - ref[:, 0]).max())
