@@ -361,9 +361,11 @@ __device__ __forceinline__ void head_of(const float* lds, int h, const float (&y
 // (kSplit, one k-step of 16), zero past column 14.  Every lane ends with z
 // of its column.  lds: the packed parameters.  mid() runs between layer 1
 // and layer 2 (dd_mlp_forward waits there for layers 2-3 of its LDS image).
-// kPipe: layer 2's split runs in the shadow of layer 3's MFMAs
-// (norm_split_next); the fused policy rollout, at the register cap, takes
-// the serial schedule.  Both give the same bits.
+// kPipe: layer 1's split runs in the shadow of layer 2's MFMAs and layer 2's
+// in that of layer 3's (norm_split_next: 65,536 rows 14.33 -> 13.93 us,
+// 262,144 rows 46.25 -> 44.21 us for the 1 -> 2 stage, lab A/B); the fused
+// policy rollout, at the register cap, takes the serial schedule.  Both give
+// the same bits.
 template <int K, bool kSplit, bool kPipe = true, typename Mid = NoMid>
 __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float (&x)[8], float (&z)[K],
                                          Mid mid = {}) {
@@ -381,9 +383,17 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
         for (int q = 0; q < 8; ++q) xs[q] = x[q] * kInScale;  // exact: a power of two
         split8(xs, b1h[0], b1l[0]);
         layer16<4, 1, kPipe>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
-        norm_relu_split<4>(acc4, lds + kV1, eps1, h, bh, bl);
-        mid();
-        layer16<4, 8, kPipe>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
+        if constexpr (kPipe) {  // layer 1's split in the shadow of layer 2's MFMAs, as 2 -> 3 below
+            mid();
+            f32x16 acc4b[4];
+            norm_split_next<4>(acc4, lds + kV1, eps1, h, a16 + kA2 / 4, lane, bh, bl, acc4b, lds + kV2 + 4 * h);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc4[t] = acc4b[t];
+        } else {
+            norm_relu_split<4>(acc4, lds + kV1, eps1, h, bh, bl);
+            mid();
+            layer16<4, 8, kPipe>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
+        }
         if constexpr (kPipe) {
             norm_split_next<2>(acc4, lds + kV2, eps2, h, a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
         } else {  // layer 2's LayerNorm + split, then all of layer 3
