@@ -417,11 +417,14 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
     head_of<K>(lds, h, y3, z);
 }
 
-// The actor's head: Sigmoid probabilities of the last layer's outputs.
+// The actor's head: Sigmoid probabilities of the last layer's outputs, as
+// v_rcp_f32(1 + v_exp_f32(-z log2 e)) (about 2 ulp; torch's 1 / (1 + expf)
+// with an IEEE division and a range-reduced expf costs ~40 more VALU per
+// drone: 65,536 rows 13.35 -> 13.09 us, lab A/B).
 __device__ __forceinline__ void actor_probs(const float (&z)[3], float (&prob)[3]) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {  // Sigmoid
-        prob[k] = 1.0f / (1.0f + expf(-z[k]));
+        prob[k] = __builtin_amdgcn_rcpf(1.0f + __expf(-z[k]));
     }
 }
 

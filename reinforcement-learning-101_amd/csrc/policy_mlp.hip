@@ -150,15 +150,36 @@ struct FwdArgs {
 // Layer 1's B operands for lane (c, h) of a tile: obs[d][8h + q] (kSplit) or
 // obs[d][2q + h], zero past column 14 and past the last row.
 template <bool kSplit>
-__device__ __forceinline__ void load_inputs(const FwdArgs& p, int64_t tile, int lane, float (&x)[8]) {
+__device__ __forceinline__ void load_inputs_raw(const FwdArgs& p, int64_t tile, int lane, float (&x)[8]) {
     const int h = lane >> 5;
     const int64_t d = tile * kCols + (lane & 31);
-    const bool live = d < p.n;
+    // branch-free: every lane loads from a valid address (row 0, column 14 for
+    // the padding), and mask_inputs zeroes what it does not own, so the loads
+    // issue back to back (a guarded load per element put each behind its own
+    // branch and a vmcnt(0): four HBM round trips in a row)
+    const float* row = p.obs + (d < p.n ? d : 0) * kIn;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int k = kSplit ? 8 * h + q : 2 * q + h;
-        x[q] = (live && k < kIn) ? p.obs[d * kIn + k] : 0.0f;
+        x[q] = row[k < kIn ? k : kIn - 1];
     }
+}
+
+template <bool kSplit>
+__device__ __forceinline__ void mask_inputs(const FwdArgs& p, int64_t tile, int lane, float (&x)[8]) {
+    const int h = lane >> 5;
+    const bool live = tile * kCols + (lane & 31) < p.n;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int k = kSplit ? 8 * h + q : 2 * q + h;
+        x[q] = (live && k < kIn) ? x[q] : 0.0f;
+    }
+}
+
+template <bool kSplit>
+__device__ __forceinline__ void load_inputs(const FwdArgs& p, int64_t tile, int lane, float (&x)[8]) {
+    load_inputs_raw<kSplit>(p, tile, lane, x);
+    mask_inputs<kSplit>(p, tile, lane, x);
 }
 
 // The actor's / critic's outputs of one drone (lane h == 0 of its column).
@@ -183,16 +204,23 @@ __device__ __forceinline__ void emit_outputs(const FwdArgs& p, int64_t d, const 
     }
 }
 
-// The LDS image arrives in two parts.  Layer 1's fragments and the vector
-// sections (13 KB) are register-staged before the block's first barrier;
-// layers 2-3 (96 KB, [kA2, kV1)) go by LDS-DMA (global_load_lds_dwordx4, 1 KB
-// per wave-instruction, the LDS image lane-linear like the packed buffer) and
-// stay in flight while every wave runs layer 1 of its first tile; the second
-// barrier, after a vmcnt(0), comes between layer 1 and layer 2 of that tile.
-// Raw s_barrier, not __syncthreads() (whose fence would drain the DMA at the
-// first barrier), and the first tile's observation is waited for before the
-// DMA is issued (hipcc waits vmcnt(0) at the first use of any ordinary load
-// made while a DMA is outstanding).
+// The LDS image arrives by LDS-DMA (global_load_lds_dwordx4, 1 KB per
+// wave-instruction, the LDS image lane-linear like the packed buffer), issued
+// right after the first tile's observation loads and before anything waits:
+// layer 1's fragments and the vector sections (13 KB) first, then layers 2-3
+// (96 KB, [kA2, kV1)).  A vmcnt that leaves the layer 2-3 pieces in flight
+// (they complete in issue order) and the block's first barrier release layer
+// 1; the second barrier, after a vmcnt(0), comes between layer 1 and layer 2
+// of the first tile, so the big part streams in behind layer 1.  Raw
+// s_barrier, not __syncthreads() (whose fence would drain the DMA at the first
+// barrier).  A buffer packed for another compute or K (its tag, kTag) gives
+// NaN outputs.  Round 5 (65,536 rows, lab A/B on one box): register-staging
+// the first 13 KB put its load latency and ds_writes ahead of the DMA issue,
+// and the observation's guarded loads went out one HBM round trip at a time
+// (13.75 -> 13.16 us with the Sigmoid below; a separate wait for layer 3's
+// pieces before layer 3 cost 0.4 us: its branch splits the scheduling region).
+constexpr size_t kLdsPad = (size_t)((kPacked + 255) / 256 * 256) * sizeof(float);  // whole 1 KB DMA pieces
+
 template <int K, bool kSplit>
 __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__ packed, FwdArgs p) {
     extern __shared__ f32x4 lds4[];
@@ -201,38 +229,86 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
     const int64_t tiles = (p.n + kCols - 1) / kCols;
     int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
     float x[8];
-    load_inputs<kSplit>(p, tile, lane, x);
-    const f32x4* src4 = reinterpret_cast<const f32x4*>(packed);
-    for (int i = threadIdx.x; i < kA2 / 4; i += kThreads) lds4[i] = src4[i];
-    for (int i = kV1 / 4 + threadIdx.x; i < kPacked / 4; i += kThreads)
-        lds4[i] = packed_fragment(src4, i, pack_tag(kSplit ? DD_MLP_F16X3 : DD_MLP_F32, K));
-    asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
-    constexpr int kChunk = 64 * 4;  // floats per wave-instruction
-    static_assert((kV1 - kA2) % kChunk == 0 && kA2 % kChunk == 0, "DMA chunks");
-    for (int q = wave; q < (kV1 - kA2) / kChunk; q += kWaves) {
-        const int off = kA2 + q * kChunk;
-        __builtin_amdgcn_global_load_lds(packed + off + lane * 4, lds4 + off / 4, 16, 0, 0);
+    f32x4 xa, xb;  // DD_MLP_F16X3's first tile: two unaligned 16 B loads, waited for with the early DMA pieces
+    if constexpr (kSplit) {
+        // columns 8h .. 8h+7 of the row from base column 7h (in bounds for
+        // h = 1; shifted down after the wait).  Inline asm so that hipcc,
+        // which waits vmcnt(0) at the first use of an ordinary load left
+        // outstanding beside an LDS-DMA, does not track them: the vmcnt(12)
+        // below covers them (they are older than every piece).
+        const int64_t d = tile * kCols + (lane & 31);
+        const float* rp = p.obs + (d < p.n ? d : 0) * kIn + 7 * h;
+        asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:16"
+                     : "=&v"(xa), "=&v"(xb)
+                     : "v"(rp)
+                     : "memory");
+    } else {
+        load_inputs<kSplit>(p, tile, lane, x);
+        // the observation is waited for before the DMA issue (see above)
+        asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int kChunk = 64 * 4;                                 // floats per wave-instruction
+    constexpr int kL1 = kA2 / kChunk;                              // layer 1: 8 pieces
+    constexpr int kEarly = kL1 + (kPacked - kV1 + kChunk - 1) / kChunk;  // + the vectors: 5, the last partial
+    constexpr int kLate = (kV1 - kA2) / kChunk;                    // layers 2-3: 96 pieces
+    static_assert(kA2 % kChunk == 0 && (kV1 - kA2) % kChunk == 0, "DMA pieces");
+    static_assert(kEarly <= 2 * kWaves && kLate % kWaves == 0, "the vmcnt below counts 12 late pieces per wave");
+    const int swave = __builtin_amdgcn_readfirstlane(wave);  // uniform: scalar branches, M0 from an SGPR
+    // Exactly two early pieces per wave, so that every wave's vmcnt below
+    // counts alike: waves past piece 12 load their first piece again, and the
+    // last vector piece's lanes past the buffer read its last float4 into the
+    // LDS pad (kLdsPad).
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int q = swave + j * kWaves < kEarly ? swave + j * kWaves : swave;
+        const int off = q < kL1 ? q * kChunk : kV1 + (q - kL1) * kChunk;
+        const int src = off + 4 * lane < kPacked ? off + 4 * lane : kPacked - 4;
+        __builtin_amdgcn_global_load_lds(packed + src, lds4 + off / 4, 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kLate / kWaves; ++j) {
+        const int off = kA2 + (swave + j * kWaves) * kChunk;
+        __builtin_amdgcn_global_load_lds(packed + off + 4 * lane, lds4 + off / 4, 16, 0, 0);
+    }
+    static_assert(kLate / kWaves == 12, "vmcnt(12)");
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // this wave's early pieces
     __builtin_amdgcn_s_barrier();
-    bool first = true;
-    const auto mid = [&first] {
-        if (first) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            first = false;
-        }
-    };
-    for (; tile < tiles; tile += (int64_t)gridDim.x * kWaves) {
-        if (!first) load_inputs<kSplit>(p, tile, lane, x);
+    if constexpr (kSplit) {
+        asm volatile("" : "+v"(xa), "+v"(xb));  // after the wait
+        const float v[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = h ? (q < 7 ? v[q + 1] : 0.0f) : v[q];
+        mask_inputs<kSplit>(p, tile, lane, x);
+    }
+    const bool tag_ok = __float_as_uint(lds[kTag]) == pack_tag(kSplit ? DD_MLP_F16X3 : DD_MLP_F32, K);
+    const auto run_tile = [&](auto mid) {
         const int64_t d = tile * kCols + c;  // this lane's drone (column)
-        const bool live = d < p.n;
         float z[K];
         mlp_body<K, kSplit>(lds, lane, x, z, mid);
-        if (!live || h != 0) continue;
+        if (d >= p.n || h != 0) return;
+        if (!tag_ok)
+#pragma unroll
+            for (int k = 0; k < K; ++k) z[k] = __builtin_nanf("");
         emit_outputs<K>(p, d, z);
+    };
+    const auto layers23 = [] {  // the second barrier: layers 2-3 in LDS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    // the first tile apart, with the second barrier between its layers 1 and
+    // 2; the loop over the others carries no barrier branch (one would split
+    // its scheduling regions)
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    if (tile < tiles) {
+        run_tile(layers23);
+        for (tile += stride; tile < tiles; tile += stride) {
+            load_inputs<kSplit>(p, tile, lane, x);
+            run_tile(NoMid{});
+        }
+    } else {
+        layers23();  // a wave without a tile still takes its part in the second barrier
     }
-    mid();  // a wave without a tile still takes its part in the second barrier
 }
 
 template <int K, bool kSplit>
@@ -240,7 +316,7 @@ hipError_t launch(const float* packed, const FwdArgs& a, hipStream_t s) {
     // the LDS image exceeds the 64 KB default; the attribute is per device, so
     // it is set on every launch (a cheap host call) rather than once per process
     const hipError_t e = hipFuncSetAttribute((const void*)mlp_kernel<K, kSplit>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPad);
     if (e != hipSuccess) return e;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -248,7 +324,7 @@ hipError_t launch(const float* packed, const FwdArgs& a, hipStream_t s) {
     const int64_t tiles = (a.n + kCols - 1) / kCols;
     const int64_t want = (tiles + kWaves - 1) / kWaves;
     const unsigned blocks = (unsigned)(want < cus ? want : cus);  // one block per CU, waves loop over tiles
-    hipLaunchKernelGGL((mlp_kernel<K, kSplit>), dim3(blocks), dim3(kThreads), kLdsBytes, s, packed, a);
+    hipLaunchKernelGGL((mlp_kernel<K, kSplit>), dim3(blocks), dim3(kThreads), kLdsPad, s, packed, a);
     return hipGetLastError();
 }
 

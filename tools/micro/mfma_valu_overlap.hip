@@ -104,7 +104,10 @@ __device__ __forceinline__ void mixed_work(int m, float* sink, int lane) {
 
 // mode 0: MFMA waves only; 1: VALU waves only; 2: both, in different waves;
 // 3: both in the same waves (waves 0-3 do MFMA then VALU in one stream);
-// 4: VALU waves only, as scalar v_fma_f32; 5 / 6: packed / scalar VALU in all 8 waves
+// 4: VALU waves only, as scalar v_fma_f32; 5 / 6: packed / scalar VALU in all 8 waves;
+// 7 / 8: interleaved (packed) in one wave / both waves of a SIMD;
+// 9: MFMA waves and scalar-VALU waves (different waves of a SIMD: does
+// scalar f32 VALU, unlike packed, run beside another wave's MFMAs?)
 __global__ __launch_bounds__(512) void k(int mode, int m, int v, float* sink) {
     extern __shared__ float big[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -116,7 +119,9 @@ __global__ __launch_bounds__(512) void k(int mode, int m, int v, float* sink) {
         if (mode == 1 || mode == 2) valu_work(v, sink, lane);
         if (mode == 4) valu_scalar_work(v, sink, lane);
         if (mode == 5) valu_work(v, sink, lane);
+        if (mode == 9) valu_scalar_work(v, sink, lane);
     }
+    if (mode == 9 && wave < 4) mfma_work(m, sink, lane);
     if (mode == 5 && wave < 4) valu_work(v, sink, lane);   // packed, both waves of a SIMD
     if (mode == 6) valu_scalar_work(v, sink, lane);         // scalar, both waves of a SIMD
     if ((mode == 7 && wave < 4) || mode == 8) {  // interleaved in one wave (7) / in both waves of a SIMD (8)
@@ -136,7 +141,7 @@ int main() {
     const int m = 2000, vs[] = {2000, 4000, 8000};
     for (int vi = 0; vi < 3; ++vi) {
         const int v = vs[vi];
-        for (int mode = 0; mode < 9; ++mode) {
+        for (int mode = 0; mode < 10; ++mode) {
             float best = 1e30f;
             for (int r = 0; r < 5; ++r) {
                 CK(hipEventRecord(e0));
