@@ -1121,7 +1121,7 @@ __global__ __launch_bounds__(kBlock) void compact_scatter_kernel(const uint8_t* 
 }
 
 #ifdef DD_ISA_PROBE
-// tools/isa_probe.sh: one kernel instantiation alone (device assembly in
+// tools/lab/isa_probe.sh: one kernel instantiation alone (device assembly in
 // seconds instead of the whole library's minutes), for reading its ISA.
 #define DD_PROBE_KERNEL_(k) template __global__ void k;
 DD_PROBE_KERNEL_(DD_ISA_PROBE)

@@ -252,14 +252,14 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
     constexpr int kEarly = kL1 + (kPacked - kV1 + kChunk - 1) / kChunk;  // + the vectors: 5, the last partial
     constexpr int kLate = (kV1 - kA2) / kChunk;                    // layers 2-3: 96 pieces
     static_assert(kA2 % kChunk == 0 && (kV1 - kA2) % kChunk == 0, "DMA pieces");
-    static_assert(kEarly <= 2 * kWaves && kLate % kWaves == 0, "the vmcnt below counts 12 late pieces per wave");
+    static_assert(kLate % kWaves == 0, "the vmcnt below counts kLate / kWaves late pieces per wave");
     const int swave = __builtin_amdgcn_readfirstlane(wave);  // uniform: scalar branches, M0 from an SGPR
-    // Exactly two early pieces per wave, so that every wave's vmcnt below
-    // counts alike: waves past piece 12 load their first piece again, and the
-    // last vector piece's lanes past the buffer read its last float4 into the
-    // LDS pad (kLdsPad).
+    // The same number of early pieces per wave (two), so that every wave's
+    // vmcnt below counts alike: waves past the last piece load their first
+    // piece again, and the last vector piece's lanes past the buffer read its
+    // last float4 into the LDS pad (kLdsPad).
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < (kEarly + kWaves - 1) / kWaves; ++j) {
         const int q = swave + j * kWaves < kEarly ? swave + j * kWaves : swave;
         const int off = q < kL1 ? q * kChunk : kV1 + (q - kL1) * kChunk;
         const int src = off + 4 * lane < kPacked ? off + 4 * lane : kPacked - 4;
@@ -270,9 +270,8 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
         const int off = kA2 + (swave + j * kWaves) * kChunk;
         __builtin_amdgcn_global_load_lds(packed + off + 4 * lane, lds4 + off / 4, 16, 0, 0);
     }
-    static_assert(kLate / kWaves == 12, "vmcnt(12)");
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // this wave's early pieces
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLate / kWaves) : "memory");  // this wave's early pieces
     __builtin_amdgcn_s_barrier();
     if constexpr (kSplit) {
         asm volatile("" : "+v"(xa), "+v"(xb));  // after the wait
