@@ -227,3 +227,25 @@ def test_f16x3_refuses_weights_beyond_f16_range(fixture, gpu_device):
     with pytest.raises(ValueError, match="f16"):
         MlpNet(sd, device=gpu_device, compute="f16x3")
     MlpNet(sd, device=gpu_device, compute="f32")  # f32 takes them
+
+
+@pytest.mark.parametrize("compute", COMPUTE)
+@pytest.mark.parametrize("n", [33, 65_536 + 37])
+def test_observations_at_any_offset(fixture, gpu_device, compute, n):
+    """The forward reads each row with unaligned loads (dd_mlp_forward's
+    prologue: two 16-byte loads per lane from column 0 or 7 of a 60-byte row).
+    Rows that start 4 or 12 bytes into an allocation, with the last row at its
+    very end, give the same bits as an aligned copy."""
+    _, nets = fixture
+    actor = MlpNet(nets["actor"], device=gpu_device, compute=compute)
+    critic = MlpNet(nets["critic"], device=gpu_device, compute=compute)
+    torch.manual_seed(n)
+    for skip in (1, 3):
+        flat = torch.randn(n * 15 + skip, device=gpu_device)
+        obs = flat[skip:].view(n, 15)  # ends exactly at the allocation's last float
+        assert obs.data_ptr() % 16 != 0
+        ref = obs.clone()
+        assert torch.equal(actor(obs), actor(ref)) and torch.equal(critic(obs), critic(ref))
+        a, lp = actor.act(obs, seed=2, step=9)
+        a2, lp2 = actor.act(ref, seed=2, step=9)
+        assert torch.equal(a, a2) and torch.equal(lp, lp2)
