@@ -53,6 +53,31 @@ __device__ __forceinline__ void valu_work(int v, float* sink, int lane) {
     if (s == 1234.5f) sink[lane] = s;
 }
 
+// mfma_work with s_nops between the MFMAs (each MFMA issues to an idle pipe:
+// does a wave stalled on a busy matrix pipe block the SIMD's issue for its
+// partner wave?).
+template <int NOPS>
+__device__ __forceinline__ void mfma_gap_work(int m, float* sink, int lane) {
+    f16x8 a = {(_Float16)1, (_Float16)lane, 0, 0, 0, 0, 0, (_Float16)0.5f};
+    f16x8 b = a;
+    f32x16 acc[4] = {};
+    for (int i = 0; i < m; ++i) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (NOPS >= 1) asm volatile("s_nop 7");
+            if constexpr (NOPS >= 2) asm volatile("s_nop 7");
+            if constexpr (NOPS >= 3) asm volatile("s_nop 7");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) s += acc[t][0] + acc[t][15];
+    if (s == 1234.5f) sink[lane] = s;
+}
+
 // The same VALU work as 16 independent scalar v_fma_f32 chains.
 __device__ __forceinline__ void valu_scalar_work(int v, float* sink, int lane) {
     float x[16];
@@ -107,7 +132,9 @@ __device__ __forceinline__ void mixed_work(int m, float* sink, int lane) {
 // 4: VALU waves only, as scalar v_fma_f32; 5 / 6: packed / scalar VALU in all 8 waves;
 // 7 / 8: interleaved (packed) in one wave / both waves of a SIMD;
 // 9: MFMA waves and scalar-VALU waves (different waves of a SIMD: does
-// scalar f32 VALU, unlike packed, run beside another wave's MFMAs?)
+// scalar f32 VALU, unlike packed, run beside another wave's MFMAs?);
+// 10: mfma_gap_work<3> waves alone; 11: mfma_gap_work<3> waves and scalar-VALU waves;
+// 12 / 13: the same with one s_nop 7 per MFMA (the pipe stays about busy)
 __global__ __launch_bounds__(512) void k(int mode, int m, int v, float* sink) {
     extern __shared__ float big[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -119,9 +146,11 @@ __global__ __launch_bounds__(512) void k(int mode, int m, int v, float* sink) {
         if (mode == 1 || mode == 2) valu_work(v, sink, lane);
         if (mode == 4) valu_scalar_work(v, sink, lane);
         if (mode == 5) valu_work(v, sink, lane);
-        if (mode == 9) valu_scalar_work(v, sink, lane);
+        if (mode == 9 || mode == 11 || mode == 13) valu_scalar_work(v, sink, lane);
     }
     if (mode == 9 && wave < 4) mfma_work(m, sink, lane);
+    if ((mode == 10 || mode == 11) && wave < 4) mfma_gap_work<3>(m, sink, lane);
+    if ((mode == 12 || mode == 13) && wave < 4) mfma_gap_work<1>(m, sink, lane);
     if (mode == 5 && wave < 4) valu_work(v, sink, lane);   // packed, both waves of a SIMD
     if (mode == 6) valu_scalar_work(v, sink, lane);         // scalar, both waves of a SIMD
     if ((mode == 7 && wave < 4) || mode == 8) {  // interleaved in one wave (7) / in both waves of a SIMD (8)
@@ -141,7 +170,7 @@ int main() {
     const int m = 2000, vs[] = {2000, 4000, 8000};
     for (int vi = 0; vi < 3; ++vi) {
         const int v = vs[vi];
-        for (int mode = 0; mode < 10; ++mode) {
+        for (int mode = 0; mode < 14; ++mode) {
             float best = 1e30f;
             for (int r = 0; r < 5; ++r) {
                 CK(hipEventRecord(e0));
