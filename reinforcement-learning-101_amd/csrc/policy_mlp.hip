@@ -221,20 +221,19 @@ __device__ __forceinline__ void emit_outputs(const FwdArgs& p, int64_t d, const 
 // pieces before layer 3 cost 0.4 us: its branch splits the scheduling region).
 constexpr size_t kLdsPad = (size_t)((kPacked + 255) / 256 * 256) * sizeof(float);  // whole 1 KB DMA pieces
 
-template <int K, bool kSplit>
-__global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__ packed, FwdArgs p) {
-    extern __shared__ f32x4 lds4[];
-    const float* lds = reinterpret_cast<const float*>(lds4);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
-    const int64_t tiles = (p.n + kCols - 1) / kCols;
-    int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
-    float x[8];
+// The prologue both forward kernels share: the first tile's observation and
+// the DMA of the LDS image, then the wait for layer 1 and the vectors and the
+// block's first barrier.  x: the first tile's layer-1 B operands.
+template <int kW, bool kSplit>
+__device__ __forceinline__ void load_image(const float* __restrict__ packed, f32x4* lds4, const FwdArgs& p,
+                                           int64_t tile, int wave, int lane, float (&x)[8]) {
+    const int h = lane >> 5;
     f32x4 xa, xb;  // DD_MLP_F16X3's first tile: two unaligned 16 B loads, waited for with the early DMA pieces
     if constexpr (kSplit) {
         // columns 8h .. 8h+7 of the row from base column 7h (in bounds for
         // h = 1; shifted down after the wait).  Inline asm so that hipcc,
         // which waits vmcnt(0) at the first use of an ordinary load left
-        // outstanding beside an LDS-DMA, does not track them: the vmcnt(12)
+        // outstanding beside an LDS-DMA, does not track them: the vmcnt
         // below covers them (they are older than every piece).
         const int64_t d = tile * kCols + (lane & 31);
         const float* rp = p.obs + (d < p.n ? d : 0) * kIn + 7 * h;
@@ -252,26 +251,26 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
     constexpr int kEarly = kL1 + (kPacked - kV1 + kChunk - 1) / kChunk;  // + the vectors: 5, the last partial
     constexpr int kLate = (kV1 - kA2) / kChunk;                    // layers 2-3: 96 pieces
     static_assert(kA2 % kChunk == 0 && (kV1 - kA2) % kChunk == 0, "DMA pieces");
-    static_assert(kLate % kWaves == 0, "the vmcnt below counts kLate / kWaves late pieces per wave");
+    static_assert(kLate % kW == 0, "the vmcnt below counts kLate / kW late pieces per wave");
     const int swave = __builtin_amdgcn_readfirstlane(wave);  // uniform: scalar branches, M0 from an SGPR
-    // The same number of early pieces per wave (two), so that every wave's
-    // vmcnt below counts alike: waves past the last piece load their first
-    // piece again, and the last vector piece's lanes past the buffer read its
-    // last float4 into the LDS pad (kLdsPad).
+    // The same number of early pieces per wave, so that every wave's vmcnt
+    // below counts alike: waves past the last piece load their first piece
+    // again, and the last vector piece's lanes past the buffer read its last
+    // float4 into the LDS pad (kLdsPad).
 #pragma unroll
-    for (int j = 0; j < (kEarly + kWaves - 1) / kWaves; ++j) {
-        const int q = swave + j * kWaves < kEarly ? swave + j * kWaves : swave;
+    for (int j = 0; j < (kEarly + kW - 1) / kW; ++j) {
+        const int q = swave + j * kW < kEarly ? swave + j * kW : swave;
         const int off = q < kL1 ? q * kChunk : kV1 + (q - kL1) * kChunk;
         const int src = off + 4 * lane < kPacked ? off + 4 * lane : kPacked - 4;
         __builtin_amdgcn_global_load_lds(packed + src, lds4 + off / 4, 16, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < kLate / kWaves; ++j) {
-        const int off = kA2 + (swave + j * kWaves) * kChunk;
+    for (int j = 0; j < kLate / kW; ++j) {
+        const int off = kA2 + (swave + j * kW) * kChunk;
         __builtin_amdgcn_global_load_lds(packed + off + 4 * lane, lds4 + off / 4, 16, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLate / kWaves) : "memory");  // this wave's early pieces
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLate / kW) : "memory");  // this wave's early pieces
     __builtin_amdgcn_s_barrier();
     if constexpr (kSplit) {
         asm volatile("" : "+v"(xa), "+v"(xb));  // after the wait
@@ -280,6 +279,23 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
         for (int q = 0; q < 8; ++q) x[q] = h ? (q < 7 ? v[q + 1] : 0.0f) : v[q];
         mask_inputs<kSplit>(p, tile, lane, x);
     }
+}
+
+// The second barrier: layers 2-3 in LDS.
+__device__ __forceinline__ void wait_layers23() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+template <int K, bool kSplit>
+__global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__ packed, FwdArgs p) {
+    extern __shared__ f32x4 lds4[];
+    const float* lds = reinterpret_cast<const float*>(lds4);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+    const int64_t tiles = (p.n + kCols - 1) / kCols;
+    int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
+    float x[8];
+    load_image<kWaves, kSplit>(packed, lds4, p, tile, wave, lane, x);
     const bool tag_ok = __float_as_uint(lds[kTag]) == pack_tag(kSplit ? DD_MLP_F16X3 : DD_MLP_F32, K);
     const auto run_tile = [&](auto mid) {
         const int64_t d = tile * kCols + c;  // this lane's drone (column)
@@ -291,10 +307,7 @@ __global__ __launch_bounds__(kThreads) void mlp_kernel(const float* __restrict__
             for (int k = 0; k < K; ++k) z[k] = __builtin_nanf("");
         emit_outputs<K>(p, d, z);
     };
-    const auto layers23 = [] {  // the second barrier: layers 2-3 in LDS
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    };
+    const auto layers23 = [] { wait_layers23(); };
     // the first tile apart, with the second barrier between its layers 1 and
     // 2; the loop over the others carries no barrier branch (one would split
     // its scheduling regions)
