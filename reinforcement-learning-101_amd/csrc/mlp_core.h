@@ -83,22 +83,29 @@ __host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r 
 // product exact, all three accumulated into ONE f32 accumulator that starts
 // at the Linear's bias — no per-layer rescale pass (round 4's lo' = (a -
 // hi) 2^11 needed the cross terms in their own pass, scaled back by 2^-11
-// with one FMA per accumulator register: 160 VALU per tile).  lo stays clear
-// of the f16 subnormals by scaling the operands by powers of two, which every
-// LayerNorm removes exactly (LN(c x) = LN(x) with eps c^2):
-//   * hidden weights x kWScale, the layer-1 input x kInScale (in registers),
-//     each LayerNorm's output x kActScale (its weight and bias, packed);
+// with one FMA per accumulator register: 160 VALU per tile).  The operands
+// are scaled by powers of two, which every LayerNorm removes exactly (LN(c x)
+// = LN(x) with eps c^2):
+//   * hidden weights x kWScale and the layer-1 input x kInScale (in
+//     registers), so that their lo halves stay clear of the f16 subnormals;
+//   * each LayerNorm's output x its act_scale (policy_mlp.hip: the power of
+//     two that keeps every output below 1, folded into its packed weight and
+//     bias), so that ReLU is the clamp modifier of the affine FMA
+//     (norm_relu_emit kClamp: 160 v_max fewer per tile; 65,536 rows 12.54 ->
+//     12.28 us, 262,144 rows 39.96 -> 38.79 us, the fused loop 12.28 -> 11.65
+//     us per frame, lab A/B).  The activations' lo halves then often sit in
+//     the f16 subnormals: the notebook models' actor probabilities within
+//     8.0e-7 of float64 and critic values within 6.9e-4 (|v| <= 850), against
+//     4.4e-7 / 2.4e-4 with activations x16 and a max() ReLU and 2.8e-7 /
+//     3.2e-4 for the centred f32 path (tools/mlp_split_sim.py --center);
 //   * each Linear's bias x kWScale x (its input's scale), each LayerNorm's
-//     eps x (that product)^2 (kEps), the last Linear's weights / kActScale.
-// Operand range: |weights| < 4094, |observations| < 1023, LayerNorm outputs
-// < 4094 (f16's 65504).  Notebook models: actor probabilities within 4.4e-7
-// of float64, critic values within 2.4e-4 (the former scheme 5.6e-7 /
-// 2.1e-4; tools/mlp_split_sim.py --single-acc).
+//     eps x (that product)^2 (kEps), the last Linear's weights / the last
+//     act_scale.
+// Operand range: |weights| < 4094, |observations| < 1023 (f16's 65504).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr float kWScale = 16.0f;    // 2^4
 constexpr float kInScale = 64.0f;   // 2^6
-constexpr float kActScale = 16.0f;  // 2^4
 
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
@@ -227,8 +234,11 @@ __device__ __forceinline__ float add_other_half(float x) {
 // then ReLU.  vec = [Linear bias | LN weight | LN bias] of 32*NT each.  Pairs
 // of registers hold adjacent rows, so the arithmetic runs as packed f32
 // (v_pk_add / v_pk_fma), in torch's form y = (x * rstd - rstd * mean) *
-// weight + bias.
-template <int NT, typename Emit, bool kBarrier = true>
+// weight + bias.  kClamp (DD_MLP_F16X3): the affine is one v_fma_f32 per row
+// with the clamp modifier, which is the ReLU because dd_mlp_pack scaled the
+// LayerNorm's weight and bias by a power of two that keeps every output below
+// 1 (act_scale, policy_mlp.hip); 160 v_max fewer per tile.
+template <int NT, typename Emit, bool kBarrier = true, bool kClamp = false>
 __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                Emit emit) {
     constexpr int kRows = 32 * NT;
@@ -266,22 +276,28 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
             const f32x2 g = *reinterpret_cast<const f32x2*>(gamma + row);
             const f32x2 b = *reinterpret_cast<const f32x2*>(beta + row);
             const f32x2 xn = __builtin_elementwise_fma(f32x2{acc[t][r], acc[t][r + 1]}, rs2, nb2);
-            const f32x2 v = __builtin_elementwise_fma(xn, g, b);
-            y[r] = fmaxf(v.x, 0.0f);  // ReLU
-            y[r + 1] = fmaxf(v.y, 0.0f);
+            if constexpr (kClamp) {  // ReLU = clamp to [0, 1] on outputs < 1: v_fma_f32 ... clamp
+                y[r] = __builtin_amdgcn_fmed3f(__builtin_fmaf(xn.x, g.x, b.x), 0.0f, 1.0f);
+                y[r + 1] = __builtin_amdgcn_fmed3f(__builtin_fmaf(xn.y, g.y, b.y), 0.0f, 1.0f);
+            } else {
+                const f32x2 v = __builtin_elementwise_fma(xn, g, b);
+                y[r] = fmaxf(v.x, 0.0f);  // ReLU
+                y[r + 1] = fmaxf(v.y, 0.0f);
+            }
         }
         emit(t, y);
         if constexpr (kBarrier) __builtin_amdgcn_sched_barrier(0);  // one tile's parameters in registers at a time
     }
 }
 
-template <int NT>
+template <int NT, bool kClamp = false>
 __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                           float (&y)[NT][16]) {
-    norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
+    auto keep = [&](int t, const float (&v)[16]) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) y[t][r] = v[r];
-    });
+    };
+    norm_relu_emit<NT, decltype(keep), true, kClamp>(acc, vec, eps, h, keep);
 }
 
 // norm_relu straight into the next layer's split B fragments: k-step s takes
@@ -290,10 +306,11 @@ __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* 
 template <int NT>
 __device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                 f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
-    norm_relu_emit<NT>(acc, vec, eps, h, [&](int t, const float (&v)[16]) {
+    auto emit = [&](int t, const float (&v)[16]) {
         split8(&v[0], bh[2 * t], bl[2 * t]);
         split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
-    });
+    };
+    norm_relu_emit<NT, decltype(emit), true, true>(acc, vec, eps, h, emit);
 }
 
 // A no-op hook (mlp_body's mid).
@@ -321,7 +338,7 @@ __device__ __forceinline__ void norm_split_next(const f32x16 (&acc)[4], const fl
             mfma3<NTO, true>([&](int to) { return a16n + (to * 8 + s) * 128; }, lane, bh[s], bl[s], out);
         }
     };
-    norm_relu_emit<4, decltype(emit), false>(acc, vec, eps, h, emit);
+    norm_relu_emit<4, decltype(emit), false, true>(acc, vec, eps, h, emit);
 }
 
 // log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
@@ -400,7 +417,7 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
             norm_relu_split<4>(acc4, lds + kV2, eps2, h, bh, bl);
             layer16<2, 8, kPipe>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
         }
-        norm_relu<2>(acc2, lds + kV3, eps3, h, y3);
+        norm_relu<2, true>(acc2, lds + kV3, eps3, h, y3);
     } else {
         float y1[4][16], y2[4][16];
         layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);

@@ -9,7 +9,10 @@ without its mean pass, as dd_mlp_pack / norm_relu_emit do (mlp_core.h kCentered)
 The `single` rows emulate the round-5 form (mlp_core.h): lo = f16(a - hi)
 unscaled, the three products in one accumulator from the bias, hidden weights
 x16, the layer-1 input x64, LayerNorm outputs x16 (powers of two the
-LayerNorms remove), centred weights."""
+LayerNorms remove), centred weights.  The `clamp` rows (the kernels since
+late round 5): every LayerNorm's output scaled by the per-layer power of two
+that keeps it below 1 (policy_mlp.hip act_scale), so that ReLU is the FMA's
+clamp modifier; lo then often sits in the f16 subnormals."""
 import sys
 
 import numpy as np
@@ -81,7 +84,7 @@ def split_unscaled(a):
 
 def fwd_single(pre, w=4, am=4, im=6):
     """The round-5 f16x3 form; the power-of-two scales of mlp_core.h (kWScale 2^w,
-    kInScale 2^im, kActScale 2^am)."""
+    kInScale 2^im, LayerNorm outputs x 2^am)."""
     f = lambda a: a.astype(np.float64)  # noqa: E731
     x = d['obs'].astype(np.float32) * np.float32(2.0 ** im)
     s_in = 2.0 ** im
@@ -110,3 +113,46 @@ for pre in ('actor', 'critic'):
         print(pre, 'single', 'max |dprob| vs f64', np.abs(p - 1 / (1 + np.exp(-ref))).max())
     else:
         print(pre, 'single', 'max |dv| vs f64', np.abs(z[:, 0] - ref[:, 0]).max())
+
+
+def act_scale(pre, j, rows):
+    """policy_mlp.hip act_scale: 2^-x with max|g| sqrt(rows) (1 + 2^-8) + max|b| = m 2^x, m in [0.5, 1)."""
+    g = np.abs(d[f'{pre}.network.{j}.weight']).max()
+    b = np.abs(d[f'{pre}.network.{j}.bias']).max()
+    bound = np.float32(g) * np.float32(np.sqrt(rows)) * np.float32(1 + 2.0 ** -8) + np.float32(b)
+    return 1.0 if not bound > 0 else float(2.0 ** -np.frexp(bound)[1])
+
+
+def fwd_clamp(pre, w=4, im=6):
+    """The clamp form: fwd_single with per-layer activation scales below 1."""
+    f = lambda a: a.astype(np.float64)  # noqa: E731
+    x = d['obs'].astype(np.float32) * np.float32(2.0 ** im)
+    s_in = 2.0 ** im
+    for (i, j), rows in zip(((0, 1), (3, 4), (6, 7)), (128, 128, 64)):
+        W, b = d[f'{pre}.network.{i}.weight'], d[f'{pre}.network.{i}.bias']
+        W = (W.astype(np.float64) - W.astype(np.float64).mean(0, keepdims=True)).astype(np.float32)
+        b = (b.astype(np.float64) - b.astype(np.float64).mean()).astype(np.float32)
+        Wh, Wl = split_unscaled(W * np.float32(2.0 ** w))
+        xh, xl = split_unscaled(x)
+        sc = np.float32(2.0 ** w * s_in)
+        acc = (f(xh) @ f(Wh).T + f(xh) @ f(Wl).T + f(xl) @ f(Wh).T + f((b * sc).astype(np.float32))).astype(np.float32)
+        z = acc * (1 / np.sqrt((acc ** 2).mean(1, keepdims=True) + np.float32(1e-5) * sc * sc))
+        s_out = act_scale(pre, j, rows)
+        g = d[f'{pre}.network.{j}.weight'].astype(np.float32) * np.float32(s_out)
+        be = d[f'{pre}.network.{j}.bias'].astype(np.float32) * np.float32(s_out)
+        v = (z * g + be).astype(np.float32)
+        assert v.max() < 1.0
+        x = np.clip(v, 0, 1).astype(np.float32)
+        s_in = s_out
+    W4 = d[f'{pre}.network.9.weight'].astype(np.float32) * np.float32(1.0 / s_in)
+    return (x @ W4.T + d[f'{pre}.network.9.bias']).astype(np.float32)
+
+
+for pre in ('actor', 'critic'):
+    ref = fwd(pre, 'f64')
+    z = fwd_clamp(pre)
+    if pre == 'actor':
+        p = 1 / (1 + np.exp(-z.astype(np.float64)))
+        print(pre, 'clamp', 'max |dprob| vs f64', np.abs(p - 1 / (1 + np.exp(-ref))).max())
+    else:
+        print(pre, 'clamp', 'max |dv| vs f64', np.abs(z[:, 0] - ref[:, 0]).max())
