@@ -46,10 +46,10 @@ constexpr size_t kLdsBytes = kPacked * sizeof(float);
 static_assert(kPacked % 4 == 0, "packed buffer is read as float4");
 
 // What dd_mlp_pack wrote the buffer for: the A sections' arithmetic
-// (DD_MLP_*) and the output width K, as the payload of a quiet NaN (0xDE:
-// the round-5 layout, scaled f16x3 sections and per-layer eps).
+// (DD_MLP_*) and the output width K, as the payload of a quiet NaN (0xDF:
+// the late round-5 layout, LayerNorm outputs at per-layer scales below 1).
 __host__ __device__ constexpr uint32_t pack_tag(int compute, int out_dim) {
-    return 0x7FC0DE00u | ((uint32_t)compute << 4) | (uint32_t)out_dim;
+    return 0x7FC0DF00u | ((uint32_t)compute << 4) | (uint32_t)out_dim;
 }
 
 // Float4 i of the packed buffer on its way into LDS.  The fragment holding
@@ -234,7 +234,7 @@ __device__ __forceinline__ float add_other_half(float x) {
 // then ReLU.  vec = [Linear bias | LN weight | LN bias] of 32*NT each.  Pairs
 // of registers hold adjacent rows, so the arithmetic runs as packed f32
 // (v_pk_add / v_pk_fma), in torch's form y = (x * rstd - rstd * mean) *
-// weight + bias.  kClamp (DD_MLP_F16X3): the affine is one v_fma_f32 per row
+// weight + bias.  kClamp (both computes): the affine is one v_fma_f32 per row
 // with the clamp modifier, which is the ReLU because dd_mlp_pack scaled the
 // LayerNorm's weight and bias by a power of two that keeps every output below
 // 1 (act_scale, policy_mlp.hip); 160 v_max fewer per tile.
@@ -421,14 +421,14 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
     } else {
         float y1[4][16], y2[4][16];
         layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
-        norm_relu<4>(acc4, lds + kV1, eps1, h, y1);
+        norm_relu<4, true>(acc4, lds + kV1, eps1, h, y1);
         mid();
         layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4,
                                lds + kV2 + 4 * h);
-        norm_relu<4>(acc4, lds + kV2, eps2, h, y2);
+        norm_relu<4, true>(acc4, lds + kV2, eps2, h, y2);
         layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2,
                                lds + kV3 + 4 * h);
-        norm_relu<2>(acc2, lds + kV3, eps3, h, y3);
+        norm_relu<2, true>(acc2, lds + kV3, eps3, h, y3);
     }
     __builtin_amdgcn_sched_barrier(0);
     head_of<K>(lds, h, y3, z);
