@@ -88,16 +88,14 @@ __host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r 
 // = LN(x) with eps c^2):
 //   * hidden weights x kWScale and the layer-1 input x kInScale (in
 //     registers), so that their lo halves stay clear of the f16 subnormals;
-//   * each LayerNorm's output x its act_scale (policy_mlp.hip: the power of
-//     two that keeps every output below 1, folded into its packed weight and
-//     bias), so that ReLU is the clamp modifier of the affine FMA
-//     (norm_relu_emit kClamp: 160 v_max fewer per tile; 65,536 rows 12.54 ->
-//     12.28 us, 262,144 rows 39.96 -> 38.79 us, the fused loop 12.28 -> 11.65
-//     us per frame, lab A/B).  The activations' lo halves then often sit in
-//     the f16 subnormals: the notebook models' actor probabilities within
-//     8.0e-7 of float64 and critic values within 6.9e-4 (|v| <= 850), against
-//     4.4e-7 / 2.4e-4 with activations x16 and a max() ReLU and 2.8e-7 /
-//     3.2e-4 for the centred f32 path (tools/mlp_split_sim.py --center);
+//   * each LayerNorm's output x kActScale (its weight and bias, packed);
+//     ReLU then happens in the split (split_pair_relu): hi rounded toward
+//     zero and raised to 0, lo = the residual clamped to [0, 1] (the FMA's
+//     clamp modifier), 160 v_max fewer per tile.  Late round 5 tried scaling
+//     the outputs below 1 instead, so that ReLU is the affine FMA's clamp:
+//     faster still, but the activations' lo halves then sit in the f16
+//     subnormals, and a layer whose LayerNorm weights spread over 10^-2..10
+//     lost ten times f32's accuracy;
 //   * each Linear's bias x kWScale x (its input's scale), each LayerNorm's
 //     eps x (that product)^2 (kEps), the last Linear's weights / the last
 //     act_scale.
@@ -106,6 +104,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr float kWScale = 16.0f;    // 2^4
 constexpr float kInScale = 64.0f;   // 2^6
+constexpr float kActScale = 16.0f;  // 2^4
 
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
@@ -126,13 +125,38 @@ __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint3
     lo = __builtin_bit_cast(uint32_t, l);
 }
 
+// split_pair of ReLU(a), ReLU(b), for a LayerNorm's outputs: hi = f16(x)
+// rounded toward zero (v_cvt_pkrtz_f16_f32) and raised to 0 (v_pk_max_f16), so
+// that for x >= 0 the residual x - hi is >= 0 and for x < 0 it is x itself;
+// lo = f16(clamp(x - hi, 0, 1)) (the residual is below 1: x < 2^11 ulp), 0 for
+// every x < 0.  RNE on the residual keeps lo unbiased; hi + lo then carries
+// about one bit less than split_pair's (tools/mlp_split_sim.py: the notebook
+// actor within 4.8e-7 of float64 against 4.4e-7).  4 VALU per pair, the ReLU
+// included (it cost two v_max).
+__device__ __forceinline__ void split_pair_relu(float a, float b, uint32_t& hi, uint32_t& lo) {
+    f16x2 h = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(a, b));
+    h = __builtin_elementwise_max(h, f16x2{(_Float16)0.0f, (_Float16)0.0f});
+    uint32_t hp = __builtin_bit_cast(uint32_t, h);
+    asm("" : "+v"(hp));
+    f32x2 r;
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0] clamp" : "=v"(r.x) : "v"(hp), "v"(a));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0] clamp" : "=v"(r.y) : "v"(hp), "v"(b));
+    const f16x2 l = {(_Float16)r.x, (_Float16)r.y};
+    hi = hp;
+    lo = __builtin_bit_cast(uint32_t, l);
+}
+
 // Eight consecutive activations (one B fragment of a k-step) -> hi, lo'.
+template <bool kRelu = false>
 __device__ __forceinline__ void split8(const float* v, f16x8& hi, f16x8& lo) {
     u32x4 h, l;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         uint32_t a, b;
-        split_pair(v[2 * m], v[2 * m + 1], a, b);
+        if constexpr (kRelu)
+            split_pair_relu(v[2 * m], v[2 * m + 1], a, b);
+        else
+            split_pair(v[2 * m], v[2 * m + 1], a, b);
         h[m] = a;
         l[m] = b;
     }
@@ -234,11 +258,14 @@ __device__ __forceinline__ float add_other_half(float x) {
 // then ReLU.  vec = [Linear bias | LN weight | LN bias] of 32*NT each.  Pairs
 // of registers hold adjacent rows, so the arithmetic runs as packed f32
 // (v_pk_add / v_pk_fma), in torch's form y = (x * rstd - rstd * mean) *
-// weight + bias.  kClamp (both computes): the affine is one v_fma_f32 per row
-// with the clamp modifier, which is the ReLU because dd_mlp_pack scaled the
-// LayerNorm's weight and bias by a power of two that keeps every output below
-// 1 (act_scale, policy_mlp.hip); 160 v_max fewer per tile.
-template <int NT, typename Emit, bool kBarrier = true, bool kClamp = false>
+// weight + bias.  kRelu: kReluMax (v_max), kReluClamp (DD_MLP_F32: the affine
+// is one v_fma_f32 per row with the clamp modifier, which is the ReLU because
+// dd_mlp_pack scaled the LayerNorm's weight and bias by a power of two that
+// keeps every output below 1, act_scale in policy_mlp.hip; the same bits, 160
+// v_max fewer per tile) or kReluInSplit (emit gets the affine's output and
+// splits it with split_pair_relu).
+enum { kReluMax = 0, kReluClamp = 1, kReluInSplit = 2 };
+template <int NT, typename Emit, bool kBarrier = true, int kRelu = kReluMax>
 __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                Emit emit) {
     constexpr int kRows = 32 * NT;
@@ -276,13 +303,13 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
             const f32x2 g = *reinterpret_cast<const f32x2*>(gamma + row);
             const f32x2 b = *reinterpret_cast<const f32x2*>(beta + row);
             const f32x2 xn = __builtin_elementwise_fma(f32x2{acc[t][r], acc[t][r + 1]}, rs2, nb2);
-            if constexpr (kClamp) {  // ReLU = clamp to [0, 1] on outputs < 1: v_fma_f32 ... clamp
+            if constexpr (kRelu == kReluClamp) {  // ReLU = clamp to [0, 1] on outputs < 1: v_fma_f32 ... clamp
                 y[r] = __builtin_amdgcn_fmed3f(__builtin_fmaf(xn.x, g.x, b.x), 0.0f, 1.0f);
                 y[r + 1] = __builtin_amdgcn_fmed3f(__builtin_fmaf(xn.y, g.y, b.y), 0.0f, 1.0f);
             } else {
                 const f32x2 v = __builtin_elementwise_fma(xn, g, b);
-                y[r] = fmaxf(v.x, 0.0f);  // ReLU
-                y[r + 1] = fmaxf(v.y, 0.0f);
+                y[r] = kRelu == kReluMax ? fmaxf(v.x, 0.0f) : v.x;  // ReLU here or in the split
+                y[r + 1] = kRelu == kReluMax ? fmaxf(v.y, 0.0f) : v.y;
             }
         }
         emit(t, y);
@@ -290,14 +317,14 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
     }
 }
 
-template <int NT, bool kClamp = false>
+template <int NT, int kRelu = kReluMax>
 __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                           float (&y)[NT][16]) {
     auto keep = [&](int t, const float (&v)[16]) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) y[t][r] = v[r];
     };
-    norm_relu_emit<NT, decltype(keep), true, kClamp>(acc, vec, eps, h, keep);
+    norm_relu_emit<NT, decltype(keep), true, kRelu>(acc, vec, eps, h, keep);
 }
 
 // norm_relu straight into the next layer's split B fragments: k-step s takes
@@ -307,10 +334,10 @@ template <int NT>
 __device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                 f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
     auto emit = [&](int t, const float (&v)[16]) {
-        split8(&v[0], bh[2 * t], bl[2 * t]);
-        split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
+        split8<true>(&v[0], bh[2 * t], bl[2 * t]);
+        split8<true>(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
     };
-    norm_relu_emit<NT, decltype(emit), true, true>(acc, vec, eps, h, emit);
+    norm_relu_emit<NT, decltype(emit), true, kReluInSplit>(acc, vec, eps, h, emit);
 }
 
 // A no-op hook (mlp_body's mid).
@@ -330,15 +357,15 @@ __device__ __forceinline__ void norm_split_next(const f32x16 (&acc)[4], const fl
                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO], const float* bias_n) {
     bias_init<NTO>(out, bias_n);
     auto emit = [&](int t, const float (&v)[16]) {
-        split8(&v[0], bh[2 * t], bl[2 * t]);
-        split8(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
+        split8<true>(&v[0], bh[2 * t], bl[2 * t]);
+        split8<true>(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int s = 2 * t + q;
             mfma3<NTO, true>([&](int to) { return a16n + (to * 8 + s) * 128; }, lane, bh[s], bl[s], out);
         }
     };
-    norm_relu_emit<4, decltype(emit), false, true>(acc, vec, eps, h, emit);
+    norm_relu_emit<4, decltype(emit), false, kReluInSplit>(acc, vec, eps, h, emit);
 }
 
 // log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
@@ -417,18 +444,18 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
             norm_relu_split<4>(acc4, lds + kV2, eps2, h, bh, bl);
             layer16<2, 8, kPipe>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
         }
-        norm_relu<2, true>(acc2, lds + kV3, eps3, h, y3);
+        norm_relu<2>(acc2, lds + kV3, eps3, h, y3);  // into the f32 head: ReLU by v_max
     } else {
         float y1[4][16], y2[4][16];
         layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);
-        norm_relu<4, true>(acc4, lds + kV1, eps1, h, y1);
+        norm_relu<4, kReluClamp>(acc4, lds + kV1, eps1, h, y1);
         mid();
         layer_mfma<4, kSteps2>(lds4 + kA2 / 4, lane, [&](int q) { return y1[q >> 4][q & 15]; }, acc4,
                                lds + kV2 + 4 * h);
-        norm_relu<4, true>(acc4, lds + kV2, eps2, h, y2);
+        norm_relu<4, kReluClamp>(acc4, lds + kV2, eps2, h, y2);
         layer_mfma<2, kSteps3>(lds4 + kA3 / 4, lane, [&](int q) { return y2[q >> 4][q & 15]; }, acc2,
                                lds + kV3 + 4 * h);
-        norm_relu<2, true>(acc2, lds + kV3, eps3, h, y3);
+        norm_relu<2, kReluClamp>(acc2, lds + kV3, eps3, h, y3);
     }
     __builtin_amdgcn_sched_barrier(0);
     head_of<K>(lds, h, y3, z);

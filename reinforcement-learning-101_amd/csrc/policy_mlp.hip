@@ -94,7 +94,7 @@ __device__ __forceinline__ float pack_a16(const DDMlpParams& p, int i) {
     return __uint_as_float(part == 0 ? hi : lo);
 }
 
-// The power of two that scales LayerNorm L's output (its weight
+// DD_MLP_F32: the power of two that scales LayerNorm L's output (its weight
 // and bias are packed times it) so that every output stays below 1, which
 // makes ReLU the clamp modifier of the affine FMA (mlp_core.h norm_relu_emit).
 // A LayerNorm output is gamma * xn + beta with |xn| < sqrt(rows) (the
@@ -143,19 +143,20 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
         const float* src[3][3] = {{p.b0, p.ln1_w, p.ln1_b}, {p.b3, p.ln4_w, p.ln4_b}, {p.b6, p.ln7_w, p.ln7_b}};
         v = o < rows ? bias_at(src[L][0], rows, o) : src[L][o / rows][o % rows];
         // the bias at its GEMM's scale (weights x input); the LN's affine at its output's
-        const float in = L == 0 ? (split ? kInScale : 1.0f) : act_scale(p, L - 1);
-        v *= o < rows ? (split ? kWScale : 1.0f) * in : act_scale(p, L);
+        const float in = L == 0 ? (split ? kInScale : 1.0f) : split ? kActScale : act_scale(p, L - 1);
+        v *= o < rows ? (split ? kWScale : 1.0f) * in : split ? kActScale : act_scale(p, L);
     } else if (i < kB4) {
         const int o = i - kW4;
         v = (o / 64) < p.out_dim ? p.w9[o] : 0.0f;
-        v *= 1.0f / act_scale(p, 2);  // the last LayerNorm's output is scaled
+        v *= 1.0f / (split ? kActScale : act_scale(p, 2));  // the last LayerNorm's output is scaled
     } else if (i < kTag) {
         const int o = i - kB4;
         v = o < p.out_dim ? p.b9[o] : (o == 3 ? p.ln_eps : 0.0f);
     } else if (i == kTag) {
         v = __uint_as_float(pack_tag(compute, p.out_dim));
     } else {  // kEps: each LayerNorm's eps at its input's scale squared
-        const float sc = (split ? kWScale : 1.0f) * (i == kEps ? (split ? kInScale : 1.0f) : act_scale(p, i - kEps - 1));
+        const float sc = split ? kWScale * (i == kEps ? kInScale : kActScale)
+                               : (i == kEps ? 1.0f : act_scale(p, i - kEps - 1));
         v = p.ln_eps * sc * sc;
     }
     out[i] = v;

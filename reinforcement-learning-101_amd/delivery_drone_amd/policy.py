@@ -76,15 +76,23 @@ class MlpNet:
         self._src = {k: torch.as_tensor(sd[k]).detach().to(device=self.device, dtype=torch.float32).contiguous()
                      for k in STATE_DICT_KEYS}
         if compute == "f16x3":
-            # the hidden Linears' weights go into f16 halves after centring over
-            # their outputs (|w - mean| <= 2 max|w|): beyond the f16 range the hi
-            # half is inf and every probability NaN, so refuse such weights here
-            # (observations and activations must stay below 65504 as well)
+            # the hidden Linears' weights go into f16 halves x16 (kWScale) after
+            # centring over their outputs (|w - mean| <= 2 max|w|): beyond the f16
+            # range the hi half is inf and every probability NaN, so refuse such
+            # weights here (observations must stay below 1023 as well)
             for k in ("0.weight", "3.weight", "6.weight"):
                 w = self._src[k]
-                if not bool(torch.isfinite(w).all()) or float(w.abs().max()) >= 65504.0 / 2:
-                    raise ValueError(f"{k}: compute='f16x3' needs finite weights below 32752 in magnitude "
-                                     "(the f16 range after centring); use compute='f32'")
+                if not bool(torch.isfinite(w).all()) or float(w.abs().max()) >= 65504.0 / 32:
+                    raise ValueError(f"{k}: compute='f16x3' needs finite weights below 2047 in magnitude "
+                                     "(the f16 range after centring and x16); use compute='f32'")
+            # each LayerNorm's output x16 is split with its ReLU (mlp_core.h
+            # split_pair_relu), which needs it below 2048: |gamma| sqrt(rows) +
+            # |beta| bounds a LayerNorm's output
+            for g, b, rows in (("1.weight", "1.bias", 128), ("4.weight", "4.bias", 128), ("7.weight", "7.bias", 64)):
+                bound = float(self._src[g].abs().max()) * rows ** 0.5 * (1 + 2 ** -8) + float(self._src[b].abs().max())
+                if not bound < 128.0:
+                    raise ValueError(f"{g}/{b}: compute='f16x3' needs LayerNorm outputs below 128 "
+                                     f"(max|weight| sqrt({rows}) + max|bias| = {bound:.4g}); use compute='f32'")
         p = abi.DDMlpParams(*[self._src[k].data_ptr() for k in STATE_DICT_KEYS], self.out_dim, self.ln_eps)
         self.packed = torch.empty(int(self._lib.dd_mlp_packed_floats()), dtype=torch.float32, device=self.device)
         abi.check(self._lib.dd_mlp_pack(ctypes.byref(p), self._mode, self.packed.data_ptr(), self._stream()),

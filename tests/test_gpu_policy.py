@@ -221,12 +221,12 @@ def test_packed_layout_tag_poisons_mismatched_launches(fixture, gpu_device):
 
 def test_f16x3_refuses_weights_beyond_f16_range(fixture, gpu_device):
     _, nets = fixture
-    sd = {k: np.array(v, copy=True) for k, v in nets["actor"].items()}
-    key = next(k for k in sd if k.endswith("3.weight"))
-    sd[key][0, 0] = 40000.0
-    with pytest.raises(ValueError, match="f16"):
-        MlpNet(sd, device=gpu_device, compute="f16x3")
-    MlpNet(sd, device=gpu_device, compute="f32")  # f32 takes them
+    for key, value in (("3.weight", 3000.0), ("4.weight", 12.0)):  # a hidden weight; a LayerNorm weight (out > 128)
+        sd = {k: np.array(v, copy=True) for k, v in nets["actor"].items()}
+        sd[next(k for k in sd if k.endswith(key))].flat[0] = value
+        with pytest.raises(ValueError, match="f16x3"):
+            MlpNet(sd, device=gpu_device, compute="f16x3")
+        MlpNet(sd, device=gpu_device, compute="f32")  # f32 takes them
 
 
 @pytest.mark.parametrize("compute", COMPUTE)
@@ -249,3 +249,47 @@ def test_observations_at_any_offset(fixture, gpu_device, compute, n):
         a, lp = actor.act(obs, seed=2, step=9)
         a2, lp2 = actor.act(ref, seed=2, step=9)
         assert torch.equal(a, a2) and torch.equal(lp, lp2)
+
+
+@pytest.mark.parametrize("compute", COMPUTE)
+@pytest.mark.parametrize("ln", ["zero_weight", "zero_all", "wide_range", "negative"])
+def test_layernorm_parameters_at_the_edges(gpu_device, compute, ln):
+    """The ReLU is no v_max: f32 scales each LayerNorm's output below 1 by a
+    power of two taken from its weight and bias (act_scale) and clamps, f16x3
+    splits the output with its ReLU (split_pair_relu).  LayerNorm weights all
+    zero (the output is the bias), weight and bias all zero (scale 1, every
+    activation 0), weights from 1e-3 to 10 in one layer, and negative weights,
+    against torch fp32."""
+    from torch import nn
+    torch.manual_seed(11)
+    for k in (3, 1):
+        layers = [nn.Linear(15, 128), nn.LayerNorm(128), nn.ReLU(), nn.Linear(128, 128), nn.LayerNorm(128), nn.ReLU(),
+                  nn.Linear(128, 64), nn.LayerNorm(64), nn.ReLU(), nn.Linear(64, k)]
+        net = nn.Sequential(*layers)
+        with torch.no_grad():
+            for i in (1, 4, 7):
+                w, b = net[i].weight, net[i].bias
+                if ln == "zero_weight":
+                    w.zero_()
+                    b.uniform_(-0.5, 0.5)
+                elif ln == "zero_all":
+                    w.zero_()
+                    b.zero_()
+                elif ln == "wide_range":
+                    w.copy_(torch.logspace(-3, 1, w.numel())[torch.randperm(w.numel())])
+                    b.uniform_(-0.2, 0.2)
+                else:
+                    w.uniform_(-1.5, -0.5)
+                    b.uniform_(-0.2, 0.2)
+        sd = net.state_dict()
+        ref = gd.torch_mlp({kk: v.numpy() for kk, v in sd.items()}, device=gpu_device)
+        got_net = MlpNet(sd, device=gpu_device, compute=compute)
+        obs = torch.randn(4097, 15, device=gpu_device) * 2.0
+        with torch.no_grad():
+            want = ref(obs)
+        got = got_net(obs)
+        if k == 1:
+            want = want[:, 0]
+        scale = float(want.abs().max()) + 1.0
+        close(got.cpu().numpy(), want.cpu().numpy(), 1e-4 if k == 1 else 0.0,
+              (1e-5 if k == 3 else 1e-4) * (scale if k == 1 else 1.0))

@@ -9,10 +9,12 @@ without its mean pass, as dd_mlp_pack / norm_relu_emit do (mlp_core.h kCentered)
 The `single` rows emulate the round-5 form (mlp_core.h): lo = f16(a - hi)
 unscaled, the three products in one accumulator from the bias, hidden weights
 x16, the layer-1 input x64, LayerNorm outputs x16 (powers of two the
-LayerNorms remove), centred weights.  The `clamp` rows (the kernels since
-late round 5): every LayerNorm's output scaled by the per-layer power of two
-that keeps it below 1 (policy_mlp.hip act_scale), so that ReLU is the FMA's
-clamp modifier; lo then often sits in the f16 subnormals."""
+LayerNorms remove), centred weights.  The `rtz` rows (the kernels since late
+round 5): the LayerNorm outputs split with their ReLU (mlp_core.h
+split_pair_relu: hi rounded toward zero and raised to 0, lo = RNE of the
+clamped residual).  The `clamp` rows (tried and dropped): every LayerNorm's
+output scaled by the per-layer power of two that keeps it below 1, so that
+ReLU is the FMA's clamp modifier; lo then often sits in the f16 subnormals."""
 import sys
 
 import numpy as np
@@ -156,3 +158,49 @@ for pre in ('actor', 'critic'):
         print(pre, 'clamp', 'max |dprob| vs f64', np.abs(p - 1 / (1 + np.exp(-ref))).max())
     else:
         print(pre, 'clamp', 'max |dv| vs f64', np.abs(z[:, 0] - ref[:, 0]).max())
+
+
+def rtz16(x):
+    h = x.astype(np.float16)
+    over = np.abs(h.astype(np.float32)) > np.abs(x)
+    return np.where(over, np.nextafter(h, np.float16(0)), h)
+
+
+def split_relu(a):
+    """split_pair_relu: hi = max(rtz16(a), 0), lo = f16(clamp(a - hi, 0, 1)) (RNE)."""
+    a = a.astype(np.float32)
+    hi = np.maximum(rtz16(a), np.float16(0))
+    return hi, np.clip(a - hi.astype(np.float32), 0, 1).astype(np.float16)
+
+
+def fwd_rtz(pre, w=4, am=4, im=6):
+    """fwd_single with the hidden activations split by split_relu (ReLU inside the split)."""
+    f = lambda a: a.astype(np.float64)  # noqa: E731
+    x = d['obs'].astype(np.float32) * np.float32(2.0 ** im)
+    s_in = 2.0 ** im
+    for n, (i, j) in enumerate(((0, 1), (3, 4), (6, 7))):
+        W, b = d[f'{pre}.network.{i}.weight'], d[f'{pre}.network.{i}.bias']
+        W = (W.astype(np.float64) - W.astype(np.float64).mean(0, keepdims=True)).astype(np.float32)
+        b = (b.astype(np.float64) - b.astype(np.float64).mean()).astype(np.float32)
+        Wh, Wl = split_unscaled(W * np.float32(2.0 ** w))
+        xh, xl = split_unscaled(x) if n == 0 else split_relu(x)
+        sc = np.float32(2.0 ** w * s_in)
+        acc = (f(xh) @ f(Wh).T + f(xh) @ f(Wl).T + f(xl) @ f(Wh).T + f((b * sc).astype(np.float32))).astype(np.float32)
+        z = acc * (1 / np.sqrt((acc ** 2).mean(1, keepdims=True) + np.float32(1e-5) * sc * sc))
+        g = d[f'{pre}.network.{j}.weight'].astype(np.float32) * np.float32(2.0 ** am)
+        be = d[f'{pre}.network.{j}.bias'].astype(np.float32) * np.float32(2.0 ** am)
+        x = (z * g + be).astype(np.float32)  # ReLU in the next split (or below, for the head)
+        s_in = 2.0 ** am
+    x = np.maximum(x, 0)
+    W4 = d[f'{pre}.network.9.weight'].astype(np.float32) * np.float32(2.0 ** -am)
+    return (x @ W4.T + d[f'{pre}.network.9.bias']).astype(np.float32)
+
+
+for pre in ('actor', 'critic'):
+    ref = fwd(pre, 'f64')
+    z = fwd_rtz(pre)
+    if pre == 'actor':
+        p = 1 / (1 + np.exp(-z.astype(np.float64)))
+        print(pre, 'rtz', 'max |dprob| vs f64', np.abs(p - 1 / (1 + np.exp(-ref))).max())
+    else:
+        print(pre, 'rtz', 'max |dv| vs f64', np.abs(z[:, 0] - ref[:, 0]).max())
