@@ -342,12 +342,15 @@ typedef struct DDMlpIO {
 } DDMlpIO;
 
 /* Arithmetic of the three hidden GEMMs.  DD_MLP_F32: the f32 MFMA, the
- * notebook's float32 model as is.  DD_MLP_F16X3 (opt-in, ~2x faster: 65,536
- * rows 35.8 -> 15-18 us on MI355X): each
- * operand split into two f16 halves, a = hi + lo * 2^-11, three f16 MFMAs
- * per product with f32 accumulation (~22 bits per product, about the f32
- * path's end-to-end error); |weights|, |obs| and activations < 65504.
- * LayerNorm, the last layer and sampling are f32 either way. */
+ * notebook's float32 model as is.  DD_MLP_F16X3 (opt-in, ~2.7x faster:
+ * 65,536 rows 33 -> 12-13 us on MI355X): each operand split into two f16
+ * halves, a = hi + lo, three f16 MFMAs per product with f32 accumulation
+ * (~21-22 bits per product, about the f32 path's end-to-end error).  Its
+ * operands must fit the f16 halves at the packing's powers of two: hidden
+ * weights |w| < 2047, observations |obs| < 1023, each LayerNorm's output
+ * below 128 (max|weight| sqrt(rows) + max|bias| < 128); beyond, results are
+ * wrong or NaN (MlpNet checks the parameters before packing).  LayerNorm,
+ * the last layer and sampling are f32 either way. */
 enum { DD_MLP_F32 = 0, DD_MLP_F16X3 = 1 };
 
 /* Floats of a packed parameter buffer (same for K = 1 and 3, either compute).
