@@ -38,7 +38,8 @@ constexpr int kV1 = kA3 + 2 * kSteps3 * 64;  // bias, LN weight, LN bias [3][128
 constexpr int kV2 = kV1 + 3 * 128;
 constexpr int kV3 = kV2 + 3 * 128;  // [3][64]
 constexpr int kW4 = kV3 + 3 * 64;   // last layer [3][64], rows >= K zero
-constexpr int kB4 = kW4 + 3 * 64;   // bias [3], LayerNorm eps
+constexpr int kB4 = kW4 + 3 * 64;   // bias [3], then kFold
+constexpr int kFold = kB4 + 3;      // DD_MLP_F16X3: bit L set = LayerNorm L folded (policy_mlp.hip fold_kernel)
 constexpr int kTag = kB4 + 4;       // layout tag [4]: pack_tag(compute, K), then the three LayerNorms' eps
 constexpr int kEps = kTag + 1;      // eps of LayerNorm 1, 2, 3 (DD_MLP_F16X3: scaled, below)
 constexpr int kPacked = kTag + 4;
@@ -265,7 +266,7 @@ __device__ __forceinline__ float add_other_half(float x) {
 // v_max fewer per tile) or kReluInSplit (emit gets the affine's output and
 // splits it with split_pair_relu).
 enum { kReluMax = 0, kReluClamp = 1, kReluInSplit = 2 };
-template <int NT, typename Emit, bool kBarrier = true, int kRelu = kReluMax>
+template <int NT, typename Emit, bool kBarrier = true, int kRelu = kReluMax, bool kFold = false>
 __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                Emit emit) {
     constexpr int kRows = 32 * NT;
@@ -307,7 +308,10 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
                 y[r] = __builtin_amdgcn_fmed3f(__builtin_fmaf(xn.x, g.x, b.x), 0.0f, 1.0f);
                 y[r + 1] = __builtin_amdgcn_fmed3f(__builtin_fmaf(xn.y, g.y, b.y), 0.0f, 1.0f);
             } else {
-                const f32x2 v = __builtin_elementwise_fma(xn, g, b);
+                // kFold (DD_MLP_F16X3, policy_mlp.hip fold_kernel): the LayerNorm's weight lives in the
+                // next layer's columns and its sign in this layer's rows; b = bias / |weight| x kActScale
+                const f32x2 v = kFold ? __builtin_elementwise_fma(f32x2{acc[t][r], acc[t][r + 1]}, rs2 * kActScale, b)
+                                      : __builtin_elementwise_fma(xn, g, b);
                 y[r] = kRelu == kReluMax ? fmaxf(v.x, 0.0f) : v.x;  // ReLU here or in the split
                 y[r + 1] = kRelu == kReluMax ? fmaxf(v.y, 0.0f) : v.y;
             }
@@ -317,27 +321,27 @@ __device__ __forceinline__ void norm_relu_emit(const f32x16 (&acc)[NT], const fl
     }
 }
 
-template <int NT, int kRelu = kReluMax>
+template <int NT, int kRelu = kReluMax, bool kFold = false>
 __device__ __forceinline__ void norm_relu(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                           float (&y)[NT][16]) {
     auto keep = [&](int t, const float (&v)[16]) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) y[t][r] = v[r];
     };
-    norm_relu_emit<NT, decltype(keep), true, kRelu>(acc, vec, eps, h, keep);
+    norm_relu_emit<NT, decltype(keep), true, kRelu, kFold>(acc, vec, eps, h, keep);
 }
 
 // norm_relu straight into the next layer's split B fragments: k-step s takes
 // registers 8(s&1)..+7 of tile s>>1 (hidden rows hid(s>>1, 8(s&1)+j, h)),
 // the k order pack_a16 assumes.  No f32 copy of the activations stays live.
-template <int NT>
+template <int NT, bool kFold>
 __device__ __forceinline__ void norm_relu_split(const f32x16 (&acc)[NT], const float* vec, float eps, int h,
                                                 f16x8 (&bh)[2 * NT], f16x8 (&bl)[2 * NT]) {
     auto emit = [&](int t, const float (&v)[16]) {
         split8<true>(&v[0], bh[2 * t], bl[2 * t]);
         split8<true>(&v[8], bh[2 * t + 1], bl[2 * t + 1]);
     };
-    norm_relu_emit<NT, decltype(emit), true, kReluInSplit>(acc, vec, eps, h, emit);
+    norm_relu_emit<NT, decltype(emit), true, kReluInSplit, kFold>(acc, vec, eps, h, emit);
 }
 
 // A no-op hook (mlp_body's mid).
@@ -351,7 +355,7 @@ struct NoMid {
 // shadow (a wave's own VALU does overlap its own MFMAs; another wave's does
 // not: tools/micro/mfma_valu_overlap.hip).  Each accumulator sees the same
 // MFMAs in the same order as layer16's, so the result is bit-identical.
-template <int NTO>
+template <int NTO, bool kFold>
 __device__ __forceinline__ void norm_split_next(const f32x16 (&acc)[4], const float* vec, float eps, int h,
                                                 const u32x4* __restrict__ a16n, int lane, f16x8 (&bh)[8],
                                                 f16x8 (&bl)[8], f32x16 (&out)[NTO], const float* bias_n) {
@@ -365,7 +369,7 @@ __device__ __forceinline__ void norm_split_next(const f32x16 (&acc)[4], const fl
             mfma3<NTO, true>([&](int to) { return a16n + (to * 8 + s) * 128; }, lane, bh[s], bl[s], out);
         }
     };
-    norm_relu_emit<4, decltype(emit), false, kReluInSplit>(acc, vec, eps, h, emit);
+    norm_relu_emit<4, decltype(emit), false, kReluInSplit, kFold>(acc, vec, eps, h, emit);
 }
 
 // log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
@@ -410,6 +414,39 @@ __device__ __forceinline__ void head_of(const float* lds, int h, const float (&y
 // 262,144 rows 46.25 -> 44.21 us for the 1 -> 2 stage, lab A/B); the fused
 // policy rollout, at the register cap, takes the serial schedule.  Both give
 // the same bits.
+// The DD_MLP_F16X3 layers up to the last LayerNorm's output y3 (ReLU'd),
+// kFold: every LayerNorm folded (fold_kernel); straight-line code either way.
+template <bool kPipe, bool kFold, typename Mid>
+__device__ __forceinline__ void split_layers(const float* lds, int lane, const float (&x)[8], float (&y3)[2][16],
+                                             Mid mid) {
+    const u32x4* a16 = reinterpret_cast<const u32x4*>(lds);
+    const int h = lane >> 5;
+    const float eps1 = lds[kEps], eps2 = lds[kEps + 1], eps3 = lds[kEps + 2];
+    f32x16 acc4[4];
+    f32x16 acc2[2];
+    f16x8 b1h[1], b1l[1], bh[8], bl[8];
+    float xs[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xs[q] = x[q] * kInScale;  // exact: a power of two
+    split8(xs, b1h[0], b1l[0]);
+    layer16<4, 1, kPipe>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
+    if constexpr (kPipe) {  // layer 1's split in the shadow of layer 2's MFMAs, as 2 -> 3 below
+        mid();
+        f32x16 acc4b[4];
+        norm_split_next<4, kFold>(acc4, lds + kV1, eps1, h, a16 + kA2 / 4, lane, bh, bl, acc4b, lds + kV2 + 4 * h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc4[t] = acc4b[t];
+        norm_split_next<2, kFold>(acc4, lds + kV2, eps2, h, a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+    } else {  // each LayerNorm + split, then all of the next layer
+        norm_relu_split<4, kFold>(acc4, lds + kV1, eps1, h, bh, bl);
+        mid();
+        layer16<4, 8, kPipe>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
+        norm_relu_split<4, kFold>(acc4, lds + kV2, eps2, h, bh, bl);
+        layer16<2, 8, kPipe>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+    }
+    norm_relu<2, kReluMax, kFold>(acc2, lds + kV3, eps3, h, y3);  // into the f32 head: ReLU by v_max
+}
+
 template <int K, bool kSplit, bool kPipe = true, typename Mid = NoMid>
 __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float (&x)[8], float (&z)[K],
                                          Mid mid = {}) {
@@ -420,31 +457,12 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
     f32x16 acc2[2];
     float y3[2][16];
     if constexpr (kSplit) {
-        const u32x4* a16 = reinterpret_cast<const u32x4*>(lds);
-        f16x8 b1h[1], b1l[1], bh[8], bl[8];
-        float xs[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) xs[q] = x[q] * kInScale;  // exact: a power of two
-        split8(xs, b1h[0], b1l[0]);
-        layer16<4, 1, kPipe>(a16 + kA1 / 4, lane, b1h, b1l, acc4, lds + kV1 + 4 * h);
-        if constexpr (kPipe) {  // layer 1's split in the shadow of layer 2's MFMAs, as 2 -> 3 below
-            mid();
-            f32x16 acc4b[4];
-            norm_split_next<4>(acc4, lds + kV1, eps1, h, a16 + kA2 / 4, lane, bh, bl, acc4b, lds + kV2 + 4 * h);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc4[t] = acc4b[t];
-        } else {
-            norm_relu_split<4>(acc4, lds + kV1, eps1, h, bh, bl);
-            mid();
-            layer16<4, 8, kPipe>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
-        }
-        if constexpr (kPipe) {
-            norm_split_next<2>(acc4, lds + kV2, eps2, h, a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
-        } else {  // layer 2's LayerNorm + split, then all of layer 3
-            norm_relu_split<4>(acc4, lds + kV2, eps2, h, bh, bl);
-            layer16<2, 8, kPipe>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
-        }
-        norm_relu<2>(acc2, lds + kV3, eps3, h, y3);  // into the f32 head: ReLU by v_max
+        // the LayerNorms folded or not (fold_kernel, all or none): one uniform
+        // branch, each side straight-line code of its own
+        if (__builtin_amdgcn_readfirstlane(__float_as_uint(lds[kFold])))
+            split_layers<kPipe, true>(lds, lane, x, y3, mid);
+        else
+            split_layers<kPipe, false>(lds, lane, x, y3, mid);
     } else {
         float y1[4][16], y2[4][16];
         layer_mfma<4, kSteps1>(lds4 + kA1 / 4, lane, [&](int q) { return x[q]; }, acc4, lds + kV1 + 4 * h);

@@ -72,11 +72,88 @@ __device__ __forceinline__ float bias_at(const float* b, int rows, int o) {
     return (float)((double)b[o] - sum / rows);
 }
 
+// ---- DD_MLP_F16X3: LayerNorm weights folded into the next layer ----------
+// gamma_j (xn_j) + beta_j = |gamma_j| (s_j xn_j + beta_j / |gamma_j|) with s_j
+// = sign(gamma_j): s_j goes into row j of the Linear before the LayerNorm (its
+// output's square sum, all the LayerNorm takes from it, does not change, and
+// the centred weights keep the mean at zero), |gamma_j| into column j of the
+// Linear after, and the affine is one FMA per activation instead of two
+// (norm_relu_emit kFold).  fold_kernel decides, into the packed slot kFold:
+// only when for every LayerNorm every |gamma_j| > 0, |beta_j / gamma_j| <= 64
+// (the x16 output stays below 2048, split_pair_relu's bound) and the next
+// hidden Linear's weights times max|gamma| stay below 2047 (the f16 range
+// after centring and x16); otherwise none is folded.
+__device__ __forceinline__ const float* ln_weight(const DDMlpParams& p, int L) {
+    return L == 0 ? p.ln1_w : L == 1 ? p.ln4_w : p.ln7_w;
+}
+__device__ __forceinline__ const float* ln_bias(const DDMlpParams& p, int L) {
+    return L == 0 ? p.ln1_b : L == 1 ? p.ln4_b : p.ln7_b;
+}
+
+__global__ __launch_bounds__(256) void fold_kernel(DDMlpParams p, float* out) {
+    __shared__ float red[3][256];
+    uint32_t flags = 0;
+    for (int L = 0; L < 3; ++L) {
+        const float* g = ln_weight(p, L);
+        const float* b = ln_bias(p, L);
+        const int rows = L == 2 ? 64 : 128;
+        float gmin = INFINITY, gmax = 0.0f, ratio = 0.0f, wmax = 0.0f;
+        for (int r = threadIdx.x; r < rows; r += 256) {
+            const float a = fabsf(g[r]);
+            gmin = fminf(gmin, a);
+            gmax = fmaxf(gmax, a);
+            ratio = fmaxf(ratio, fabsf(b[r]) / a);  // inf or NaN when a == 0: gmin rules that out
+        }
+        if (L < 2) {  // the next hidden Linear: [64 or 128][128]
+            const float* w = L == 0 ? p.w3 : p.w6;
+            const int n = (L == 0 ? 128 : 64) * 128;
+            for (int i = threadIdx.x; i < n; i += 256) wmax = fmaxf(wmax, fabsf(w[i]));
+        }
+        red[0][threadIdx.x] = -gmin;
+        red[1][threadIdx.x] = fmaxf(gmax, 0.0f);
+        red[2][threadIdx.x] = ratio;
+        __syncthreads();
+        for (int k = 128; k > 0; k >>= 1) {
+            if (threadIdx.x < k)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + k]);
+            __syncthreads();
+        }
+        const float gmin_all = -red[0][0], gmax_all = red[1][0], ratio_all = red[2][0];
+        __syncthreads();
+        red[0][threadIdx.x] = wmax;
+        __syncthreads();
+        for (int k = 128; k > 0; k >>= 1) {
+            if (threadIdx.x < k) red[0][threadIdx.x] = fmaxf(red[0][threadIdx.x], red[0][threadIdx.x + k]);
+            __syncthreads();
+        }
+        const float wmax_all = red[0][0];
+        __syncthreads();
+        const bool ok = gmin_all > 0.0f && ratio_all <= 64.0f && (L == 2 || wmax_all * gmax_all < 2047.0f);
+        flags |= ok ? 1u << L : 0u;
+    }
+    // all or none: the kernels branch once per tile, between two straight-line bodies
+    if (threadIdx.x == 0) out[kFold] = __uint_as_float(flags == 7u ? 7u : 0u);
+}
+
+// The packed value's fold factors: s_j for row j of the Linear before
+// LayerNorm L (L = the layer's own index), |gamma_j| for column j of the
+// Linear after LayerNorm L.
+__device__ __forceinline__ bool folded(const float* out, int L) {
+    return (__float_as_uint(out[kFold]) >> L) & 1u;
+}
+__device__ __forceinline__ float row_sign(const DDMlpParams& p, const float* out, int L, int row) {
+    return folded(out, L) && ln_weight(p, L)[row] < 0.0f ? -1.0f : 1.0f;
+}
+__device__ __forceinline__ float col_gain(const DDMlpParams& p, const float* out, int L, int col) {
+    return folded(out, L) ? fabsf(ln_weight(p, L)[col]) : 1.0f;
+}
+
 // DD_MLP_F16X3 A fragments, one packed float = two halves: section
 // [tile][k-step][hi | lo'][lane][8 halves]; lane l of k-step s of out tile t
 // holds W[32t + (l&31)][k] for its elements j, k = 8h + j (layer 1) or hidden
 // row hid(s>>1, 8(s&1) + j, h) (layers 2, 3: the B fragments split_acts makes).
-__device__ __forceinline__ float pack_a16(const DDMlpParams& p, int i) {
+__device__ __forceinline__ float pack_a16(const DDMlpParams& p, const float* out, int i) {
     const int base = i < kA2 ? kA1 : i < kA3 ? kA2 : kA3;
     const int ks = base == kA1 ? 1 : 8;
     const int o = i - base;
@@ -87,7 +164,10 @@ __device__ __forceinline__ float pack_a16(const DDMlpParams& p, int i) {
     for (int e = 0; e < 2; ++e) {
         const int j = 2 * m + e;
         const int col = base == kA1 ? 8 * h + j : hid(s >> 1, 8 * (s & 1) + j, h);
-        v[e] = weight_at(p, base, row, col) * kWScale;  // exact: a power of two
+        const int L = base == kA1 ? 0 : base == kA2 ? 1 : 2;  // this Linear feeds LayerNorm L
+        float f = row_sign(p, out, L, row);  // and takes LayerNorm L - 1's outputs
+        if (L > 0) f *= col_gain(p, out, L - 1, col);
+        v[e] = weight_at(p, base, row, col) * f * kWScale;  // kWScale: exact, a power of two
     }
     uint32_t hi, lo;
     split_pair(v[0], v[1], hi, lo);
@@ -125,7 +205,7 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
     const bool split = compute == DD_MLP_F16X3;
     float v = 0.0f;
     if (i < kV1 && compute == DD_MLP_F16X3) {
-        v = pack_a16(p, i);
+        v = pack_a16(p, out, i);
     } else if (i < kV1) {  // A operands: lane l of k-step q of out tile t holds W[32t + (l&31)][k(q, l>>5)]
         const int base = i < kA2 ? kA1 : i < kA3 ? kA2 : kA3;
         const int steps = i < kA2 ? kSteps1 : i < kA3 ? kSteps2 : kSteps3;
@@ -142,16 +222,22 @@ __global__ void pack_kernel(DDMlpParams p, int32_t compute, float* out) {
         const int o = i - (L == 0 ? kV1 : L == 1 ? kV2 : kV3);
         const float* src[3][3] = {{p.b0, p.ln1_w, p.ln1_b}, {p.b3, p.ln4_w, p.ln4_b}, {p.b6, p.ln7_w, p.ln7_b}};
         v = o < rows ? bias_at(src[L][0], rows, o) : src[L][o / rows][o % rows];
+        if (split && o < rows) v *= row_sign(p, out, L, o);                       // folded: the row's sign
+        if (split && o >= 2 * rows && folded(out, L)) v /= fabsf(src[L][1][o % rows]);  // beta / |gamma|
         // the bias at its GEMM's scale (weights x input); the LN's affine at its output's
         const float in = L == 0 ? (split ? kInScale : 1.0f) : split ? kActScale : act_scale(p, L - 1);
         v *= o < rows ? (split ? kWScale : 1.0f) * in : split ? kActScale : act_scale(p, L);
     } else if (i < kB4) {
         const int o = i - kW4;
         v = (o / 64) < p.out_dim ? p.w9[o] : 0.0f;
+        if (split) v *= col_gain(p, out, 2, o % 64);
         v *= 1.0f / (split ? kActScale : act_scale(p, 2));  // the last LayerNorm's output is scaled
+    } else if (i == kFold) {  // fold_kernel's flags (DD_MLP_F16X3), none for f32
+        if (!split) out[i] = 0.0f;
+        return;
     } else if (i < kTag) {
         const int o = i - kB4;
-        v = o < p.out_dim ? p.b9[o] : (o == 3 ? p.ln_eps : 0.0f);
+        v = o < p.out_dim ? p.b9[o] : 0.0f;
     } else if (i == kTag) {
         v = __uint_as_float(pack_tag(compute, p.out_dim));
     } else {  // kEps: each LayerNorm's eps at its input's scale squared
@@ -382,6 +468,8 @@ int dd_mlp_pack(const DDMlpParams* p, int32_t compute, float* packed, void* stre
     for (const float* q : req)
         if (!q) return hipErrorInvalidValue;
     const int threads = 256, blocks = (dd::mlp::kPacked + threads - 1) / threads;
+    if (compute == DD_MLP_F16X3)  // which LayerNorms fold into the next layer, before the packing reads it
+        hipLaunchKernelGGL(dd::mlp::fold_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *p, packed);
     hipLaunchKernelGGL(dd::mlp::pack_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, *p, compute, packed);
     return hipGetLastError();
 }
