@@ -372,16 +372,19 @@ __device__ __forceinline__ void norm_split_next(const f32x16 (&acc)[4], const fl
     norm_relu_emit<4, decltype(emit), false, kReluInSplit, kFold>(acc, vec, eps, h, emit);
 }
 
-// log p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
-// as torch's Bernoulli does (probs_to_logits, clamp_probs): log p or
-// log(1 - p).  (torch evaluates it as -BCE-with-logits of the logit; the two
-// agree to float32 rounding.)
-__device__ __forceinline__ float bernoulli_logp(float p, bool on) {
+// p(y) of one Bernoulli factor, probabilities clamped to [eps, 1 - eps]
+// as torch's Bernoulli does (probs_to_logits, clamp_probs), whose log_prob
+// is log p or log(1 - p) (torch evaluates it as -BCE-with-logits of the
+// logit; the two agree to float32 rounding).
+// Here the factor's probability itself, p or 1 - p (1 - p rounded once: exact
+// for p >= 1/2, else within 2^-24 of it); actor_sample takes ONE logf of the
+// three factors' product (each >= FLT_EPSILON, so the product is a normal
+// float) instead of a logf per factor (round 2 had already cut a select
+// between logf and log1pf that evaluated both, ~90 VALU per tile; one logf
+// instead of three: 65,536 rows 12.61 -> 12.46 us, lab A/B).
+__device__ __forceinline__ float bernoulli_factor(float p, bool on) {
     const float pc = fminf(fmaxf(p, FLT_EPSILON), 1.0f - FLT_EPSILON);
-    // one logf per factor: log(1 - p) with 1 - p rounded once (exact for p >= 1/2,
-    // else within 2^-24 of log1p(-p)) instead of a select between logf and
-    // log1pf, which evaluated both (~90 VALU per 32-drone tile)
-    return logf(on ? pc : 1.0f - pc);
+    return on ? pc : 1.0f - pc;
 }
 
 
@@ -500,14 +503,15 @@ __device__ __forceinline__ void actor_sample(const float (&prob)[3], uint64_t en
     philox4x32_10((uint32_t)env, (uint32_t)(env >> 32), (uint32_t)step, (uint32_t)(step >> 32) ^ 0x5A5A5A5Au,
                   (uint32_t)seed, (uint32_t)(seed >> 32), r);
     bits = 0;
-    lp = 0.0f;
+    float pr = 1.0f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float u = (float)(r[k] >> 8) * 0x1p-24f;  // uniform [0, 1), 24 bits
         const bool on = u < prob[k];
         bits |= on ? (1u << k) : 0u;
-        lp += bernoulli_logp(prob[k], on);
+        pr *= bernoulli_factor(prob[k], on);
     }
+    lp = logf(pr);  // log of the product: the sum of the factors' logs to float32 rounding
     // a NaN probability (packed_fragment's poison) makes the log-probability
     // NaN too: the clamped Bernoulli log-probability alone would hide it
     lp = fmaf(prob[0] + prob[1] + prob[2], 0.0f, lp);
