@@ -415,8 +415,8 @@ __device__ __forceinline__ void head_of(const float* lds, int h, const float (&y
 // kPipe: layer 1's split runs in the shadow of layer 2's MFMAs and layer 2's
 // in that of layer 3's (norm_split_next: 65,536 rows 14.33 -> 13.93 us,
 // 262,144 rows 46.25 -> 44.21 us for the 1 -> 2 stage, lab A/B); the fused
-// policy rollout, at the register cap, takes the serial schedule.  Both give
-// the same bits.
+// policy rollout, at the register cap, pipelines the 2 -> 3 stage only.  Every
+// schedule gives the same bits.
 // The DD_MLP_F16X3 layers up to the last LayerNorm's output y3 (ReLU'd),
 // kFold: every LayerNorm folded (fold_kernel); straight-line code either way.
 template <bool kPipe, bool kFold, typename Mid>
@@ -440,12 +440,13 @@ __device__ __forceinline__ void split_layers(const float* lds, int lane, const f
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc4[t] = acc4b[t];
         norm_split_next<2, kFold>(acc4, lds + kV2, eps2, h, a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
-    } else {  // each LayerNorm + split, then all of the next layer
+    } else {  // layer 1's LayerNorm + split, then all of layer 2; layer 2's split in layer 3's shadow
+        // (the fused rollout, at the register cap: 11.84 -> 11.60 us per frame for the 2 -> 3 stage,
+        // 13 VGPRs spilled; the 1 -> 2 stage as well spilled more and ran slower, lab A/B)
         norm_relu_split<4, kFold>(acc4, lds + kV1, eps1, h, bh, bl);
         mid();
         layer16<4, 8, kPipe>(a16 + kA2 / 4, lane, bh, bl, acc4, lds + kV2 + 4 * h);
-        norm_relu_split<4, kFold>(acc4, lds + kV2, eps2, h, bh, bl);
-        layer16<2, 8, kPipe>(a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
+        norm_split_next<2, kFold>(acc4, lds + kV2, eps2, h, a16 + kA3 / 4, lane, bh, bl, acc2, lds + kV3 + 4 * h);
     }
     norm_relu<2, kReluMax, kFold>(acc2, lds + kV3, eps3, h, y3);  // into the f32 head: ReLU by v_max
 }
