@@ -47,6 +47,8 @@ def parse():
                    help="seconds of CPU-baseline wall time per leg (0 = skip)")
     p.add_argument("--cpu-workers", type=int, default=0,
                    help="CPU-baseline processes per leg (0 = this process's CPU share: host_cpu_share())")
+    p.add_argument("--cpu-baseline-json", default="",
+                   help="(set by the N > 1 launcher) a cpu_baseline already measured, for rank 0 to report")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
@@ -289,6 +291,8 @@ def hbm_point(n, precision, seed, dev, write_obs, allocs=3, rounds=6):
            "placements": {"allocations": len(runs), "us_per_step_by_allocation": [round(t * 1e3, 1) for t in per_alloc],
                           "frac_by_allocation": [round(bpe * n / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                                  for t in per_alloc],
+                          "frac_min": round(bpe * n / (max(per_alloc) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "frac_max": round(bpe * n / (min(per_alloc) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                           "value": "median over allocations"},
            "traffic": pmc_traffic(n, precision, write_obs), "bytes_per_env": bpe}
     del runs, rows
@@ -346,6 +350,8 @@ def rollout_point(n, frames, precision, seed, dev, warm=120, timed=40):
            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_env_frame": fbytes, "bytes_per_launch": total,
            "timing": {"warm_launches": warm, "timed_launches": timed,
                       "ms_steady_median": round(ms, 4), "ms_steady_mean": round(statistics.mean(steady), 4),
+                      "ms_all_mean": round(statistics.mean(ms_all), 4),
+                      "frac_all_mean": round(total / (statistics.mean(ms_all) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "ms_first5_median": round(statistics.median(ms_all[:5]), 4),
                       "ms_transient_max": round(max(ms_all[:warm]), 4),
                       "rule": "median of the timed launches after the warm ones (DVFS transient excluded)"},
@@ -811,21 +817,78 @@ def socket_point(seed, dev, steps=2000):
             "reference_published": "300-500 steps/s (delivery_drone/SOCKET_API.md:373)"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` (N > 1) outside torch.distributed.run: this
+    process is the launcher, not a rank.  It touches no GPU (a device count
+    initialises nothing on this image), runs the CPU baseline once, then starts
+    N fresh ranks as a child `torch.distributed.run` (a child process, never an
+    exec), hands rank 0 the baseline through a file and relays rank 0's JSON
+    line.  Returns the children's exit code."""
+    import subprocess
+    import tempfile
+    if args.dist_backend == "nccl":
+        import torch
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} with --dist-backend nccl but {ndev} visible GPUs: "
+                             "RCCL needs one GPU per rank")
+    cpu_file = None
+    if args.cpu_baseline > 0:
+        share = host_cpu_share()
+        cpu = cpu_baseline(args.cpu_baseline, args.cpu_workers or share["cores"], args.seed, share)
+        fd, cpu_file = tempfile.mkstemp(prefix="dd_cpu_baseline_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(cpu, f)
+    argv = [a for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv + \
+          ["--cpu-baseline", "0"] + (["--cpu-baseline-json", cpu_file] if cpu_file else [])
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DD_BENCH_LAUNCHER="1")
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    finally:
+        if cpu_file:
+            os.unlink(cpu_file)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    for ln in r.stdout.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if r.returncode == 0 and len(lines) != 1:
+        print(f"expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    for ln in lines:
+        print(ln, flush=True)
+    return r.returncode
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
         args.gpus = world
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline > 0:
+    if rank == 0 and args.cpu_baseline > 0:
+        # before any GPU call (the legs fork worker processes); at N > 1 under
+        # torch.distributed.run the other ranks wait in the rendezvous meanwhile
         share = host_cpu_share()
         workers = args.cpu_workers or share["cores"]
         cpu = cpu_baseline(args.cpu_baseline, workers, args.seed, share)
+    elif rank == 0 and args.cpu_baseline_json:
+        with open(args.cpu_baseline_json) as f:
+            cpu = json.load(f)
+        cpu["measured_by"] = "the launcher process (bench.py --gpus N), before the ranks started"
 
     import torch
     import torch.distributed as dist
@@ -871,35 +934,62 @@ def main():
     # K = 20, W = 5: four 5-launch replays leave gaps, profiles/r02/k20.)
     G = min(args.graph_steps, max(args.steps, 1))
     graphs = {}
+    # The kernels' own span: timing events recorded as event nodes INSIDE the
+    # timed graphs (external events), one at the head of the first graph of
+    # the timed region and one at the tail of its last.  They bracket the K
+    # step kernels only, not the host's graph submission before the first
+    # one (at K = 20 that submission gap sat inside the stream events below
+    # and priced launch overhead into roofline.frac: VERDICT r05 #1).
+    ev_head = torch.cuda.Event(enable_timing=True, external=True)
+    ev_tail = torch.cuda.Event(enable_timing=True, external=True)
+    seq = ([G] * (args.steps // G) + ([args.steps % G] if args.steps % G else [])) if G > 0 else []
+    timed = [(k, j == 0, j == len(seq) - 1) for j, k in enumerate(seq)]
 
-    def graph_of(k: int):
-        if k not in graphs:
+    def graph_of(k: int, head: bool = False, tail: bool = False):
+        key = (k, head, tail)
+        if key not in graphs:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=stream):
+                if head:
+                    ev_head.record(stream)
                 for i in range(k):
                     env.step(rows[i % args.action_rows], write_obs=write_obs)
-            graphs[k] = g
-        return graphs[k]
+                if tail:
+                    ev_tail.record(stream)
+            graphs[key] = g
+        return graphs[key]
 
     with torch.cuda.stream(stream):
         if G > 0:
             for _ in range(3):  # settle allocations before capture
                 one_step()
             torch.cuda.synchronize(dev)
-            for k in {G, args.steps % G, args.warmup % G} - {0}:
+            for k in {G, args.warmup % G} - {0}:
                 graph_of(k)
+            for key in set(timed):
+                graph_of(*key)
 
-        def run(k: int):
+        def run_warmup(k: int):
             if G <= 0:
                 for _ in range(k):
                     one_step()
                 return
             for _ in range(k // G):
-                graphs[G].replay()
+                graphs[(G, False, False)].replay()
             if k % G:
-                graphs[k % G].replay()
+                graphs[(k % G, False, False)].replay()
 
-        run(args.warmup)
+        def run_timed():
+            if G <= 0:
+                ev_head.record(stream)
+                for _ in range(args.steps):
+                    one_step()
+                ev_tail.record(stream)
+                return
+            for key in timed:
+                graphs[key].replay()
+
+        run_warmup(args.warmup)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -908,7 +998,7 @@ def main():
         ev1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
-        run(args.steps)
+        run_timed()
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -916,8 +1006,9 @@ def main():
             torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    kernel_ms = ev_head.elapsed_time(ev_tail)
 
-    wall, gpu_ms = reduce_max([wall, gpu_ms], args.dist_backend, dev)
+    wall, gpu_ms, kernel_ms = reduce_max([wall, gpu_ms, kernel_ms], args.dist_backend, dev)
 
     # sanity: the batch is alive and finite
     assert torch.isfinite(env.obs).all().item() and int(env.episode.max()) >= 1
@@ -950,13 +1041,15 @@ def main():
         sp = socket_point(args.seed, dev)
         rp = render_point(args.seed, dev)
 
+    pg_world = dist.get_world_size() if use_pg else 1
     if rank == 0:
-        total_steps = n * world * args.steps
+        total_steps = n * pg_world * args.steps
         value = total_steps / wall
-        step_ms = gpu_ms / args.steps  # device time per launch on the kernel's stream
+        step_ms = kernel_ms / args.steps  # the K step kernels' own span per launch
         bytes_env = env.step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=write_obs)
         traffic, traffic_note = pmc_traffic_row(n, args.precision, write_obs)
         achieved = bytes_env * n / (step_ms * 1e-3) / 1e9
+        stream_achieved = bytes_env * n / (gpu_ms / args.steps * 1e-3) / 1e9
         roof = {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -966,14 +1059,21 @@ def main():
             "traffic": traffic,
             "traffic_note": traffic_note,
             "bytes_per_env": bytes_env,
-            "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, false>",
-            "timing": "HIP events on the launch stream over the K timed steps / K",
+            "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, 0>",
+            "us_per_launch": round(step_ms * 1e3, 4),
+            "timing": ("HIP timing events recorded as nodes inside the timed hipGraphs, at the head of the first "
+                       "and the tail of the last: the K step kernels' span / K (the host's graph submission "
+                       "excluded; max over ranks)"),
+            "stream_events": {"us_per_launch": round(gpu_ms / args.steps * 1e3, 4),
+                              "frac": round(stream_achieved / HBM_PEAK_GBS, 4),
+                              "note": "events on the stream around the graph launches (includes the submission "
+                                      "gap before the first kernel)"},
         }
         out = {
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "env-steps/s",
-            "n_gpus": world,
+            "n_gpus": pg_world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall * 1e3 / args.steps, 6),
@@ -987,13 +1087,16 @@ def main():
                              "N GPUs = N x 262144 (config 4 at N=8)" if n == 262_144 else
                              f"{n} drones per GPU, randomised spawn + auto-reset"),
                 "envs_per_gpu": n,
-                "global_envs": n * world,
+                "global_envs": n * pg_world,
                 "storage": args.precision,
                 "compute": "f64 (reference arithmetic, rounded once on store)",
                 "obs": "[N,15] f32 every step" if write_obs else "off",
                 "actions": "u8 bitmask [N]",
                 "launch": f"hipGraph of {G} steps" if G > 0 else "eager",
-                "parallelism": f"env-shard x{world} (no collective on the step path)",
+                "parallelism": f"env-shard x{pg_world} (no collective on the step path)",
+                "world_size_source": ("torch.distributed.get_world_size()" if use_pg else "single process"),
+                "launch_form": ("bench.py --gpus N launcher -> torch.distributed.run" if os.environ.get("DD_BENCH_LAUNCHER")
+                                else "torch.distributed.run" if "RANK" in os.environ else "plain"),
             },
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -1016,6 +1119,7 @@ def main():
             "socket_point": sp,
             "render_point": rp,
             "gpu_ms_per_step": round(step_ms, 6),
+            "stream_ms_per_step": round(gpu_ms / args.steps, 6),
             "device": torch.cuda.get_device_name(dev),
             "build_info": abi.lib().dd_build_info().decode(),
         }

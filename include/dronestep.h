@@ -260,8 +260,9 @@ int dd_rollout(const DDConfig *cfg, const DDState *st, const DDRolloutIO *io,
 int dd_rollout_kernel(const DDConfig *cfg, const DDState *st, const DDRolloutIO *io,
                       int64_t n);
 
-/* Sticky error bits the kernels set on the device (DD_ERR_*), read
- * synchronously (the device is synchronised) and cleared if `clear`. */
+/* Sticky error bits the kernels set on the device (DD_ERR_*), read after a
+ * hipDeviceSynchronize (work on every stream, non-blocking ones included, has
+ * finished) and cleared if `clear`. */
 enum { DD_ERR_HANDOVER = 1 }; /* a split-rollout hand-over wait ran out: rows of
                                  that launch are not to be trusted */
 int dd_device_errors(uint32_t *bits, int32_t clear);

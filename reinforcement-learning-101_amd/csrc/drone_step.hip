@@ -1383,7 +1383,12 @@ int dd_rollout_kernel(const DDConfig* cfg, const DDState* st, const DDRolloutIO*
 
 int dd_device_errors(uint32_t* bits, int32_t clear) {
     if (!bits) return hipErrorInvalidValue;
-    hipError_t e = hipMemcpyFromSymbol(bits, HIP_SYMBOL(dd::dd_error_bits), sizeof(uint32_t), 0, hipMemcpyDeviceToHost);
+    // every stream's work first: torch's side streams do not synchronise with
+    // the null stream, so a launch still running there could set its bit
+    // after this read and be blamed on a later check
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return (int)e;
+    e = hipMemcpyFromSymbol(bits, HIP_SYMBOL(dd::dd_error_bits), sizeof(uint32_t), 0, hipMemcpyDeviceToHost);
     if (e == hipSuccess && clear) {
         static const uint32_t zero = 0;
         e = hipMemcpyToSymbol(HIP_SYMBOL(dd::dd_error_bits), &zero, sizeof(uint32_t), 0, hipMemcpyHostToDevice);

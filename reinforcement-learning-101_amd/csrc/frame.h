@@ -669,7 +669,7 @@ __device__ __forceinline__ double reinforce_reward(const double v[13], uint32_t 
     const double vx = v[2], vy = v[3], angle = v[4], fuel = v[6], dist = v[9], dx = v[10], dy = v[11],
                  speed = v[12];
     // time penalty: -inverse_quadratic(dist, decay=50, scaler=1-0.3) - 0.3
-    constexpr double kScale = 1.0 - 0.3;  // (0.7000000000000001, as Python forms it)
+    constexpr double kScale = 1.0 - 0.3;  // 0.69999999999999996 = RN(0.7), as Python forms 1 - 0.3
     const double time_penalty = -(kScale * (1.0 / (1.0 + (50.0 * (dist * dist))))) - 0.3;
     // calc_velocity_alignment: only its sign is used
     const double odx0 = -dx, ody0 = -dy;

@@ -100,7 +100,9 @@ __host__ __device__ constexpr int hid(int t, int r, int h) { return 32 * t + (r 
 //   * each Linear's bias x kWScale x (its input's scale), each LayerNorm's
 //     eps x (that product)^2 (kEps), the last Linear's weights / the last
 //     act_scale.
-// Operand range: |weights| < 4094, |observations| < 1023 (f16's 65504).
+// Operand range: |weights| < 2047 before centring (< 4094 after; MlpNet,
+// dronestep.h and fold_kernel check the first), |observations| < 1023
+// (f16's 65504).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr float kWScale = 16.0f;    // 2^4
@@ -484,7 +486,10 @@ __device__ __forceinline__ void mlp_body(const float* lds, int lane, const float
 }
 
 // The actor's head: Sigmoid probabilities of the last layer's outputs, as
-// v_rcp_f32(1 + v_exp_f32(-z log2 e)) (about 2 ulp; torch's 1 / (1 + expf)
+// v_rcp_f32(1 + v_exp_f32(-z log2 e)).  Its error grows with |z|: for
+// z < 0, p ~ exp(z) and the rounding of z*log2(e) alone is a relative error
+// of about |z| * 2^-24, i.e. ~|z| f32 ulps of p (~20 ulps at z = -15, a
+// log-probability error near 1e-6); a few ulps for |z| < 2 (torch's 1 / (1 + expf)
 // with an IEEE division and a range-reduced expf costs ~40 more VALU per
 // drone: 65,536 rows 13.35 -> 13.09 us, lab A/B).
 __device__ __forceinline__ void actor_probs(const float (&z)[3], float (&prob)[3]) {

@@ -332,6 +332,26 @@ def test_split_rollout_handover_timeout_is_reported(gpu_device):
     env.check_device_errors()  # read and cleared
 
 
+def test_device_errors_wait_for_side_streams(gpu_device):
+    """dd_device_errors synchronises the device, so a no_wait
+    rollout still queued on a non-blocking torch stream (behind a ~20 ms spin
+    there) has run and set its bit before check_device_errors() reads it, with
+    no synchronize by the caller."""
+    n = 65_532
+    env = VecDroneEnv(n, device=gpu_device, config=EnvConfig(randomize_drone=True, auto_reset=True, seed=5))
+    env.reset()
+    env.check_device_errors()
+    acts = torch.randint(0, 8, (64, n), device=gpu_device, dtype=torch.uint8)
+    torch.cuda.synchronize(gpu_device)
+    side = torch.cuda.Stream(gpu_device)
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(50_000_000)
+        env.rollout(acts, kernel="no_wait")
+    with pytest.raises(abi.NativeLibraryError, match="DD_ERR_HANDOVER"):
+        env.check_device_errors()
+    env.check_device_errors()
+
+
 def test_rollout_kernel_single_equals_split(gpu_device):
     """kernel="single" keeps the single-role kernel where the split one
     applies; both equal the same frames bit for bit."""

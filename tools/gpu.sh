@@ -11,6 +11,8 @@
 #   smoke      __graft_entry__.smoke()
 #   bench20    the driver's line: bench.py --gpus 1 --steps 20 --warmup 5
 #   bench      bench.py with its defaults (every extra point)
+#   prof20     rocprofv3 --kernel-trace --stats of the driver's exact command (bench.py --gpus 1 --steps 20
+#              --warmup 5) and the trace summary of its 20 timed config-3 launches (c3_k20_trace_summary.json)
 #   prof       rocprofv3 kernel traces: config 3, the 16.8M HBM point, the extra points
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the step kernel at 262,144 and 16.8M drones
 #   sq         SQ instruction counters of the step / rollout kernels (tools/pmc_sq.sh)
@@ -43,6 +45,11 @@ run_step() {
     bench)
         timeout -k 10 600 python bench.py ${BENCHARGS} > $OUT/bench_default.json 2> $OUT/bench_default.err \
             && python3 tools/bench_summary.py $OUT/bench_default.json ;;
+    prof20)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_k20 -o bench -f csv -- python3 bench.py \
+            --gpus 1 --steps 20 --warmup 5 > $OUT/prof_k20_bench.json 2> $OUT/prof20.err || return 1
+        python3 tools/trace_summary.py $OUT/prof_k20/bench_kernel_trace.csv --kernel "step_kernel<float, 0, true, 0>" \
+            --grid 262144 --slice 8:28 > $OUT/c3_k20_trace_summary.json && cut -c1-300 $OUT/c3_k20_trace_summary.json ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3 -o bench -f csv -- python3 bench.py \
             --steps 2000 --warmup 200 --cpu-baseline 0 --hbm-point 0 --rollout-point 0 --no-extra-points \
