@@ -6,7 +6,7 @@ set -e
 OUT=${1:?out.s}
 K=${2:-"rollout_kernel<float, 0, true, true, false>(RolloutArgs, Soa<float>)"}
 shift; [ $# -gt 0 ] && shift
-cd "$(dirname "$0")/../reinforcement-learning-101_amd"
+cd "$(dirname "$0")/../../reinforcement-learning-101_amd"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Wall -Ibuild -I../include \
   --offload-device-only -S "-DDD_ISA_PROBE=$K" "$@" -o "$OUT" csrc/drone_step.hip 2>&1 | grep -v "unused during compilation" || true
 SYM=$(grep -o '^_ZN2dd[A-Za-z0-9_]*:' "$OUT" | head -1 | tr -d ':')
