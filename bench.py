@@ -213,12 +213,15 @@ def cpu_baseline(seconds: float, workers: int, seed: int, share: dict | None = N
 
 # ------------------------------------------------------------------- GPU bench
 class KernelSpanEvents:
-    """Two HIP timing events recorded as EVENT NODES inside captured hipGraphs
-    (hipEventRecordWithFlags(..., hipEventRecordExternal) during capture; torch
-    refuses external events on ROCm, so the HIP runtime torch itself loaded is
-    called through ctypes).  Recorded at the head of the first timed graph and
-    the tail of the last, they bracket the step kernels only: the host's graph
-    submission before the first kernel is outside (VERDICT r05 #1)."""
+    """Two HIP timing events recorded by EVENT-RECORD NODES inside the timed
+    hipGraphs: after capture (torch.cuda.CUDAGraph(keep_graph=True)) a node
+    recording `head` is added before the graph's root nodes and one recording
+    `tail` after its leaves (hipGraphAddEventRecordNode /
+    hipGraphAddDependencies on raw_cuda_graph()), then the graph is
+    instantiated.  Recorded in the first and the last timed graph they bracket
+    the step kernels only; the host's graph submission before the first kernel
+    is outside.  torch refuses external events on ROCm, so the
+    HIP runtime torch itself loaded is called through ctypes."""
 
     def __init__(self):
         import ctypes
@@ -243,11 +246,38 @@ class KernelSpanEvents:
         if rc != 0:
             raise RuntimeError(f"{what} failed: hipError {rc}")
 
+    def _nodes(self, fn, *lead):
+        c = self.c
+        n = c.c_size_t(0)
+        self._check(fn(*lead, None, c.byref(n)), fn.__name__)
+        arr = (c.c_void_p * max(1, n.value))()
+        self._check(fn(*lead, arr, c.byref(n)), fn.__name__)
+        return [c.c_void_p(arr[i]) for i in range(n.value)]
+
+    def add_nodes(self, graph, head: bool, tail: bool) -> None:
+        """Event-record nodes into a captured, not yet instantiated graph."""
+        c, hip = self.c, self.hip
+        g = c.c_void_p(graph.raw_cuda_graph())
+        if tail:
+            leaves = [nd for nd in self._nodes(hip.hipGraphGetNodes, g)
+                      if not self._nodes(hip.hipGraphNodeGetDependentNodes, nd)]
+            deps = (c.c_void_p * len(leaves))(*[nd.value for nd in leaves])
+            node = c.c_void_p()
+            self._check(hip.hipGraphAddEventRecordNode(c.byref(node), g, deps, c.c_size_t(len(leaves)), self.tail),
+                        "hipGraphAddEventRecordNode(tail)")
+        if head:
+            roots = self._nodes(hip.hipGraphGetRootNodes, g)
+            node = c.c_void_p()
+            self._check(hip.hipGraphAddEventRecordNode(c.byref(node), g, None, c.c_size_t(0), self.head),
+                        "hipGraphAddEventRecordNode(head)")
+            for r in roots:
+                self._check(hip.hipGraphAddDependencies(g, c.byref(node), c.byref(r), c.c_size_t(1)),
+                            "hipGraphAddDependencies")
+
     def record(self, which: str, stream) -> None:
-        """Inside a capture: an event-record node; outside: an ordinary record."""
+        """An ordinary record on the stream (the eager path)."""
         ev = self.head if which == "head" else self.tail
-        self._check(self.hip.hipEventRecordWithFlags(ev, self.c.c_void_p(stream.cuda_stream), self.c.c_uint(1)),
-                    "hipEventRecordWithFlags(External)")
+        self._check(self.hip.hipEventRecord(ev, self.c.c_void_p(stream.cuda_stream)), "hipEventRecord")
 
     def elapsed_ms(self) -> float:
         ms = self.c.c_float(0.0)
@@ -995,14 +1025,13 @@ def main():
     def graph_of(k: int, head: bool = False, tail: bool = False):
         key = (k, head, tail)
         if key not in graphs:
-            g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph(keep_graph=head or tail)
             with torch.cuda.graph(g, stream=stream):
-                if head:
-                    spans.record("head", stream)
                 for i in range(k):
                     env.step(rows[i % args.action_rows], write_obs=write_obs)
-                if tail:
-                    spans.record("tail", stream)
+            if head or tail:
+                spans.add_nodes(g, head, tail)
+                g.instantiate()
             graphs[key] = g
         return graphs[key]
 
