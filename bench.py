@@ -1082,8 +1082,32 @@ def main():
             torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    kernel_ms = spans.elapsed_ms()
+    span_ms = spans.elapsed_ms()
     spans.close()
+    # The event-record nodes cost a fixed ~10 us per head/tail pair on top of
+    # the kernels (tools/lab/graph_event_probe.py: span = 10.5 us + N x 7.9 us
+    # over N = 1..40 kernels, and a graph holding only the two nodes spans the
+    # same 10.5 us).  So an untimed graph of the two nodes alone, replayed
+    # after the timed region, measures that overhead and it is subtracted.
+    marker_ms = 0.0
+    if G > 0:
+        import statistics
+        import warnings
+        cal = KernelSpanEvents()
+        gc = torch.cuda.CUDAGraph(keep_graph=True)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")  # "The CUDA Graph is empty": it holds only the two event nodes
+            with torch.cuda.graph(gc, stream=stream):
+                pass
+        cal.add_nodes(gc, True, True)
+        gc.instantiate()
+        cals = []
+        for _ in range(7):
+            gc.replay()
+            cals.append(cal.elapsed_ms())
+        cal.close()
+        marker_ms = statistics.median(cals)
+    kernel_ms = span_ms - marker_ms
 
     wall, gpu_ms, kernel_ms = reduce_max([wall, gpu_ms, kernel_ms], args.dist_backend, dev)
 
@@ -1139,8 +1163,10 @@ def main():
             "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, 0>",
             "us_per_launch": round(step_ms * 1e3, 4),
             "timing": ("HIP timing events recorded as nodes inside the timed hipGraphs, at the head of the first "
-                       "and the tail of the last: the K step kernels' span / K (the host's graph submission "
-                       "excluded; max over ranks)"),
+                       "and the tail of the last: (their span - the span of a graph of the two nodes alone) / K, "
+                       "the K step kernels' own time (the host's graph submission excluded; max over ranks)"),
+            "span_us": round(span_ms * 1e3, 2),
+            "marker_overhead_us": round(marker_ms * 1e3, 2),
             "stream_events": {"us_per_launch": round(gpu_ms / args.steps * 1e3, 4),
                               "frac": round(stream_achieved / HBM_PEAK_GBS, 4),
                               "note": "events on the stream around the graph launches (includes the submission "
@@ -1226,17 +1252,20 @@ def pmc_traffic_row(n: int, precision: str, obs: bool, path: str | None = None, 
     except (OSError, ValueError):
         return None, "no profiles/pmc_traffic.json"
     have = abi.lib().dd_build_info().decode()
-    step_isa = dict(kv.split("=", 1) for kv in have.split(";")).get("step_isa")
+    mine = dict(kv.split("=", 1) for kv in have.split(";"))
     for r in rows.get("rows", []):
         if (r.get("envs") == n and r.get("precision") == precision and r.get("obs") == obs
                 and r.get("kernel", "step_kernel") == kernel and r.get("frames") == frames):
             got = r.get("build_info")
             if not got:
                 return None, "PMC row has no build_info (measured on an older build)"
-            if dict(kv.split("=", 1) for kv in got.split(";")).get("step_isa") != step_isa:
-                return None, f"PMC row measured on step_isa of '{got}', this library is '{have}'"
+            theirs = dict(kv.split("=", 1) for kv in got.split(";"))
+            # the kernel's own ISA hash when both builds carry it (tools/build_info.py), else the whole unit's
+            key = f"{kernel}_isa" if f"{kernel}_isa" in theirs and f"{kernel}_isa" in mine else "step_isa"
+            if theirs.get(key) != mine.get(key):
+                return None, f"PMC row measured on {key} of '{got}', this library is '{have}'"
             return r.get("hbm_bytes_per_launch"), (f"PMC FETCH_SIZE/WRITE_SIZE passes of the {kernel}; its ISA "
-                                                   f"(step_isa={step_isa}) matches this library's")
+                                                   f"({key}={mine.get(key)}) matches this library's")
     return None, f"no PMC row for {kernel} envs={n} precision={precision} obs={obs} frames={frames}"
 
 

@@ -46,11 +46,11 @@ typedef struct OraLane {
     int32_t steps, episode;
 } OraLane;
 
-/* ---- Philox4x32-10 -------------------------------------------------------*/
-void ora_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+/* ---- Philox4x32-R: 10 rounds (actions, policy samples), 7 (spawns) -------*/
+static void philox4x32_r(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4], int rounds) {
     uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
     uint32_t k0 = key[0], k1 = key[1];
-    for (int round = 0; round < 10; ++round) {
+    for (int round = 0; round < rounds; ++round) {
         uint64_t a = (uint64_t)0xD2511F53u * c0;
         uint64_t b = (uint64_t)0xCD9E8D57u * c2;
         uint32_t n0 = (uint32_t)(b >> 32) ^ c1 ^ k0;
@@ -63,6 +63,15 @@ void ora_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
         k1 += 0xBB67AE85u;
     }
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+void ora_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    philox4x32_r(ctr, key, out, 10);
+}
+
+/* The spawn stream (frame.h spawn_words): Philox4x32-7 since round 6. */
+void ora_philox4x32_7(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    philox4x32_r(ctr, key, out, 7);
 }
 
 static int32_t pick(uint32_t r, int32_t lo, uint32_t span) {
@@ -99,7 +108,7 @@ void ora_spawn(const DDConfig *c, int64_t env, OraLane *s) {
     uint32_t ctr[4] = {(uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)s->episode, 0u};
     uint32_t key[2] = {(uint32_t)c->seed, (uint32_t)(c->seed >> 32)};
     uint32_t r[4];
-    ora_philox4x32_10(ctr, key, r);
+    ora_philox4x32_7(ctr, key, r);
     if (c->randomize_drone) {
         s->x = pick(r[0], c->drone_x_min, (uint32_t)(c->drone_x_max - c->drone_x_min + 1));
         s->y = pick(r[1], c->drone_y_min, (uint32_t)(c->drone_y_max - c->drone_y_min + 1));

@@ -59,6 +59,8 @@ def lib() -> ctypes.CDLL:
                 h.ora_probe.argtypes = [cfgp, stp, P, P, ctypes.c_int64]
                 h.ora_philox4x32_10.argtypes = [P, P, P]
                 h.ora_philox4x32_10.restype = None
+                h.ora_philox4x32_7.argtypes = [P, P, P]
+                h.ora_philox4x32_7.restype = None
                 h.ora_bench.argtypes = [cfgp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
                 h.ora_gae.argtypes = [P, P, P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_double]
                 h.ora_gae.restype = None
@@ -76,6 +78,15 @@ def philox4x32_10(ctr, key):
     k = np.ascontiguousarray(key, dtype=np.uint32)
     out = np.zeros(4, dtype=np.uint32)
     lib().ora_philox4x32_10(_p(c), _p(k), _p(out))
+    return out
+
+
+def philox4x32_7(ctr, key):
+    """The spawn stream's generator (drone_oracle.c ora_spawn, frame.h spawn_words)."""
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().ora_philox4x32_7(_p(c), _p(k), _p(out))
     return out
 
 

@@ -40,9 +40,10 @@ R_STEP, R_LAND, R_CRASH, R_FUEL, R_OOB = -0.1, 100.0, -100.0, -50.0, -50.0
 _M32 = 0xFFFFFFFF
 
 
-def philox4x32_10(c0, c1, c2, c3, k0, k1):
-    """Philox4x32-10 (Salmon et al., SC'11) on Python ints (oracle/drone_oracle.c)."""
-    for _ in range(10):
+def philox4x32_10(c0, c1, c2, c3, k0, k1, rounds=10):
+    """Philox4x32-10 (Salmon et al., SC'11) on Python ints (oracle/drone_oracle.c);
+    rounds=7: the spawn stream."""
+    for _ in range(rounds):
         p0 = 0xD2511F53 * c0
         p1 = 0xCD9E8D57 * c2
         c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & _M32, p1 & _M32, ((p0 >> 32) ^ c3 ^ k1) & _M32, p0 & _M32
@@ -153,7 +154,8 @@ class Game:
     def reset(self):
         self.episode += 1
         e, s = self.env_id, self.seed
-        r = philox4x32_10(e & _M32, (e >> 32) & _M32, self.episode & _M32, 0, s & _M32, (s >> 32) & _M32)
+        r = philox4x32_10(e & _M32, (e >> 32) & _M32, self.episode & _M32, 0, s & _M32, (s >> 32) & _M32,
+                          rounds=7)
         if self.randomize_drone:
             self.craft = Craft(100 + ((r[0] * 601) >> 32), 50 + ((r[1] * 201) >> 32))
         else:

@@ -750,6 +750,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
     // (profiles/r04/lab/roll_spawn_ahead.jsonl)
     constexpr bool kAhead = AFMT != DD_ACT_PHILOX;
     SpawnAhead ahead;
+    ThrustTrig tt;  // the thrust's sin / cos of the lane's current angle (frame.h next_trig)
     // One frame; kObs and kAuto (auto_reset) are compile-time so the loop
     // body carries no uniform branch on them.
     auto run_frame = [&](const int f, uint32_t& slot, auto obs_c, auto auto_c) __attribute__((always_inline)) {
@@ -774,7 +775,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
         double reward;
         const bool was_done = (s.status & DD_ST_DONE) != 0;
         auto fast = [&]() __attribute__((always_inline)) {
-            return frame_checked<kRef, true, kSplit>(k, sw, act, s);  // kSplit: the writer finishes it
+            return frame_checked<kRef, true, kSplit, true>(k, sw, act, s, &tt);  // kSplit: the writer finishes it
         };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
@@ -853,6 +854,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
         if constexpr (kObs && !kSplit) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
         // the obs above sees the unrounded frame, like dd_step's
         quantize<T, kRef>(s);
+        next_trig(s, tt);  // frame f + 1's thrust rotation, beside the rest of this frame
         if constexpr (kObs && !kSplit) {
             if constexpr (kHeld) {
                 store_held_wave(held, rsrc_over(obs_prev, prev_bytes));  // frame f - 1's rows
@@ -872,6 +874,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
     };
     auto run = [&](auto obs_c, auto auto_c) __attribute__((always_inline)) {
         if constexpr (decltype(auto_c)::value && kAhead) ahead.init(sw, env, s.episode);
+        next_trig(s, tt);
         // an odd count leaves the loop between the pair's frames (`break`, not
         // a skipped second frame): the loop latch is then reached from one
         // path only, and the vmcnt the compiler derives there for the

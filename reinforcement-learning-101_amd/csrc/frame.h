@@ -212,9 +212,12 @@ __device__ __forceinline__ double measure(Lane& s) {
 // a rollout's frame loop issues no scalar load that a join's lgkmcnt wait
 // would couple to its LDS reads); s.episode becomes the value after
 // `episode += 1`.
-// The Philox block of (seed; env, episode) that a re-spawn draws from.
+// The Philox block of (seed; env, episode) that a re-spawn draws from:
+// Philox4x32-7 (philox.h; 10 rounds until round 5 — the step kernel's re-spawn
+// branch runs in ~35 % of its waves at config 3, and the three rounds were
+// 1.8 % of the step, lab A/B profiles/r06/lab/).
 __device__ __forceinline__ void spawn_words(const DDConfig& c, int64_t env, int32_t episode, uint32_t (&r)[4]) {
-    philox4x32_10((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)episode, 0u, (uint32_t)c.seed,
+    philox4x32_7((uint32_t)env, (uint32_t)((uint64_t)env >> 32), (uint32_t)episode, 0u, (uint32_t)c.seed,
                   (uint32_t)(c.seed >> 32), r);
 }
 
@@ -332,8 +335,22 @@ __device__ __forceinline__ double wrap_angle(double a) {
 // landing test's speed limit compares the squared speed (9 = 3^2: for every
 // squared speed outside the risky edge band, sqrt(ss) > 3 iff ss > 9; NaN
 // fails both).  s.speed, s.dist and s.total are stale on return.
-template <bool kRef, bool kFlat, bool kExact = false, bool kDefer = false>
-__device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s, bool* risky_out) {
+// The thrust's sin and cos of a lane's angle, computed ahead (kPipe).  In a
+// loop that keeps the state in registers the thrust of frame f + 1 rotates by
+// the angle frame f stored (rounded to the storage width), which is known
+// halfway through frame f: the sincos for frame f + 1 (next_trig) then runs
+// beside the rest of frame f, off the chain from the angle to vx', x' and the
+// flags.  Same function of the same angle: the frame's values are bit for bit
+// those of the sincos taken inside it.
+struct ThrustTrig {
+    double s, c;
+};
+__device__ __forceinline__ void next_trig(const Lane& s, ThrustTrig& t) { sincos_deg<false>(s.angle, &t.s, &t.c); }
+
+template <bool kRef, bool kFlat, bool kExact = false, bool kDefer = false, bool kPipe = false>
+__device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s, bool* risky_out,
+                                        const ThrustTrig* tt = nullptr) {
+    static_assert(!kPipe || (kFlat && !kExact), "the pipelined thrust trig is the loops' fast frame");
     static_assert(!kDefer || (kRef && kFlat && !kExact), "deferred frames: reference world, rollout form");
     const DDConfig& c = k.c;
 
@@ -359,7 +376,12 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     const bool main_on = (act & 1u) && s.fuel > 0.0;
     if constexpr (kFlat) {
         double sa, ca, dvx, dvy;
-        sincos_deg<kExact>(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
+        if constexpr (kPipe) {
+            sa = tt->s;
+            ca = tt->c;
+        } else {
+            sincos_deg<kExact>(s.angle, &sa, &ca);  // rotate_point(0, -MAIN_THRUST_POWER, angle)   physics.py:6-23
+        }
         thrust(sa, ca, &dvx, &dvy);
         s.vx = main_on ? s.vx + dvx : s.vx;
         s.vy = main_on ? s.vy + dvy : s.vy;
@@ -449,8 +471,13 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     bool on_pad = false;  // _check_landing: bottom centre on the platform, slow and upright
     const double rx = c.platform_half_width + fabs(c.drone_half_height);
     const double ry = c.platform_half_height + fabs(c.drone_half_height);
-    const double slack = 1.0 + 1e-9 * (fabs(s.x) + fabs(s.y) + fabs(s.px) + fabs(s.py) + rx + ry);
-    const bool near_pad = upright && fabs(s.x - s.px) <= rx + slack && fabs(s.y - s.py) <= ry + slack;
+    // |bx - x| <= |half_height| + the rounding of bx, and the rounding of bx,
+    // px and their difference stays below 2^-50 (|x| + |px| + |bx - px|) + 1
+    // ulp-scale terms: with |px| <= |x| + rx + 1 that is far inside the
+    // 2^-30 |x| + 1 of slack taken here (x - px: one rounding; NaN or an
+    // infinite x fails the test, as the reference's comparisons fail)
+    const bool near_pad = upright && fma(-fabs(s.x), 0x1p-30, fabs(s.x - s.px)) <= rx + 1.0 &&
+                          fma(-fabs(s.y), 0x1p-30, fabs(s.y - s.py)) <= ry + 1.0;
     if (near_pad) {
         // (lanes out of this reach of the pad: on_pad = false exactly as the
         // reference's comparisons give, the bottom centre lying within
@@ -472,10 +499,21 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
             risky |= edge;
         }
         if (slow) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
-            double sb, cb;
-            sincos_deg<kExact, kSgpr>(s.angle, &sb, &cb);
-            const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
-            const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
+            double sb, cb, bx, by;
+            if constexpr (kRef && !kExact) {
+                // upright (|angle| <= 20): the small-angle sin / cos, within
+                // 3e-13 (trig.h); bx, by then lie within 1e-11 of the
+                // reference's, far inside the risky band below
+                static_assert(reference_config().max_landing_angle == 20.0 &&
+                              reference_config().drone_half_height == 10.0, "sincos_upright_deg's range");
+                trig::sincos_upright_deg<kSgpr>(s.angle, &sb, &cb);
+                bx = s.x - c.drone_half_height * sb;
+                by = s.y + c.drone_half_height * cb;
+            } else {
+                sincos_deg<kExact, kSgpr>(s.angle, &sb, &cb);
+                bx = s.x + (0.0 * cb - c.drone_half_height * sb);
+                by = s.y + (0.0 * sb + c.drone_half_height * cb);
+            }
             on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
                      (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
             if constexpr (!kExact) {
@@ -562,11 +600,12 @@ __device__ __forceinline__ double finish_deferred(Lane& s, bool was_done, bool a
 // from the kept state with glibc's functions (a wave-uniform rare branch; as
 // an out-of-line call, or through an LDS slot, it measured slower or equal,
 // DESIGN.md §3.2).
-template <bool kRef, bool kFlat, bool kDefer = false>
-__device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s) {
+template <bool kRef, bool kFlat, bool kDefer = false, bool kPipe = false>
+__device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s,
+                                                const ThrustTrig* tt = nullptr) {
     const Lane s0 = s;
     bool risky = false;
-    double reward = frame<kRef, kFlat, false, kDefer>(k, sw, act, s, &risky);
+    double reward = frame<kRef, kFlat, false, kDefer, kPipe>(k, sw, act, s, &risky, tt);
     if (__builtin_expect(__ballot(risky) != 0, 0)) {
         if (risky) {
             s = s0;

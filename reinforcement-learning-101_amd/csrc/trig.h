@@ -109,6 +109,27 @@ DD_HD inline void sincos(double x, double* s, double* c) {
     *c = ((n + 1) & 2) ? -b : b;
 }
 
+// (sin x, cos x) of x = deg * (pi/180) for |deg| <= 20 (an upright drone,
+// config.py's max landing angle) by Taylor polynomials with no range
+// reduction: sin to x^9, cos to x^8, so |error| <= |x|^11/11! + rounding
+// < 3e-13 (sin) and |x|^10/10! < 8e-12 (cos) at |x| <= 0.3491.  Not the
+// reference's sin/cos to the ulp: only for the landing test's bottom
+// centre, which decides on_pad by comparisons whose risky band (2^-19
+// relative, frame.h) is ~10^6 times wider than 10 x this error, so every
+// decision outside the band is the reference's and the band is redone with
+// glibc's functions.  ~11 VALU instead of the general sincos's ~35.
+constexpr double kT3 = -1.0 / 6.0, kT5 = 1.0 / 120.0, kT7 = -1.0 / 5040.0, kT9 = 1.0 / 362880.0;
+constexpr double kT2 = -0.5, kT4 = 1.0 / 24.0, kT6 = -1.0 / 720.0, kT8 = 1.0 / 40320.0;
+template <bool kSgpr = false>
+DD_HD inline void sincos_upright_deg(double deg, double* s, double* c) {
+    const double x = deg * (3.14159265358979323846 / 180.0);
+    const double z = x * x;
+    const double ps = hstep_c<kSgpr>(kT3, z, hstep_c<kSgpr>(kT5, z, hstep(kT7, z, kT9)));
+    *s = fma(x * z, ps, x);
+    const double pc = hstep_c<kSgpr>(kT2, z, hstep_c<kSgpr>(kT4, z, hstep(kT6, z, kT8)));
+    *c = fma(z, pc, 1.0);
+}
+
 #if defined(__HIPCC__)
 // sqrt(x), correctly rounded, for x >= 2^-767, +-0, +inf and NaN: the
 // instruction sequence ROCm's compiler emits for a double sqrt on gfx950

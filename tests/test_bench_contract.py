@@ -77,7 +77,17 @@ def test_pmc_traffic_only_for_the_measured_build(tmp_path):
     assert v is None and "step_isa" in note
     p.write_text(json.dumps({"rows": [dict(row, build_info=info)]}))
     v, note = b.pmc_traffic_row(262144, "f32", True, str(p))
-    assert v == 123 and info.split(";")[1] in note  # the note names the matched step ISA
+    mine = dict(kv.split("=", 1) for kv in info.split(";"))
+    assert v == 123 and f"step_kernel_isa={mine['step_kernel_isa']}" in note  # the note names the matched hash
+    # the step kernel's own hash decides: another edit of the translation unit (step_isa) keeps the row
+    other = ";".join(f"{k}={'0' * 16 if k == 'step_isa' else v}" for k, v in mine.items())
+    p.write_text(json.dumps({"rows": [dict(row, build_info=other)]}))
+    assert b.pmc_traffic_row(262144, "f32", True, str(p))[0] == 123
+    other = ";".join(f"{k}={'0' * 16 if k == 'step_kernel_isa' else v}" for k, v in mine.items())
+    p.write_text(json.dumps({"rows": [dict(row, build_info=other)]}))
+    v, note = b.pmc_traffic_row(262144, "f32", True, str(p))
+    assert v is None and "step_kernel_isa" in note
+    p.write_text(json.dumps({"rows": [dict(row, build_info=info)]}))
     assert b.pmc_traffic_row(4096, "f32", True, str(p))[0] is None
     # rollout rows are keyed by kernel and frames, and never stand in for a step row (or the reverse)
     roll = dict(row, envs=65536, kernel="rollout_kernel", frames=256, hbm_bytes_per_launch=456, build_info=info)

@@ -218,6 +218,30 @@ def test_oracle_reset_ranges_match_reference():
     assert list(np.concatenate([obs64[0, 2:7], obs64[0, 12:]])) == facts["reset_obs_tail"]
 
 
+def test_spawn_stream_is_philox_7_rounds():
+    # round 6: spawns draw from Philox4x32-7 (frame.h spawn_words); actions and
+    # policy samples keep 10 rounds.  The C oracle, the Python-object CPU
+    # baseline (oracle/pyloop.py) and the round count agree.
+    from oracle import pyloop
+    rng = np.random.default_rng(7)
+    for _ in range(64):
+        c = [int(x) for x in rng.integers(0, 2**32, 4, dtype=np.uint64)]
+        k = [int(x) for x in rng.integers(0, 2**32, 2, dtype=np.uint64)]
+        assert list(ora.philox4x32_7(c, k)) == list(pyloop.philox4x32_10(*c, *k, rounds=7))
+        assert list(ora.philox4x32_10(c, k)) == list(pyloop.philox4x32_10(*c, *k))
+        assert list(ora.philox4x32_7(c, k)) != list(ora.philox4x32_10(c, k))
+    # a spawn is the 7-round block of (env, episode + 1; seed)
+    from delivery_drone_amd.config import EnvConfig
+    cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=0x1234_5678_9ABC)
+    env = ora.OracleEnv(8, config=cfg, env_id_base=1000)
+    env.reset()
+    for j in range(8):
+        e = 1000 + j
+        r = ora.philox4x32_7([e & 0xFFFFFFFF, e >> 32, 1, 0], [cfg.seed & 0xFFFFFFFF, cfg.seed >> 32])
+        assert env.x[j] == cfg.drone_x_min + ((int(r[0]) * (cfg.drone_x_max - cfg.drone_x_min + 1)) >> 32)
+        assert env.py[j] == cfg.platform_y_lo + ((int(r[3]) * (cfg.platform_y_hi - cfg.platform_y_lo)) >> 32)
+
+
 def test_oracle_reset_uniformity_chi2():
     """Spawn draws are uniform over the reference's integer ranges."""
     n = 200_000

@@ -1,8 +1,9 @@
-"""Emit build/build_info.cpp: dd_build_info() returns the ABI version and the
-sha256 of the device ISA of the step translation unit (drone_step.hip, the
-kernels whose PMC traffic profiles/pmc_traffic.json records) and of the fused
-policy rollout, so a counter summary can be tied to the exact code it was
-measured on (bench.py compares them before reporting roofline.traffic)."""
+"""Emit build/build_info.cpp: dd_build_info() returns the ABI version, the
+sha256 of the device ISA of the step translation unit (drone_step.hip) and of
+the fused policy rollout, and of the step and rollout kernels' own function
+bodies (step_kernel_isa, rollout_kernel_isa), so a counter summary can be tied
+to the exact code it was measured on (bench.py compares the row's kernel hash
+before reporting roofline.traffic / rollout_point.traffic)."""
 import hashlib
 import sys
 
@@ -17,8 +18,30 @@ def digest(path: str) -> str:
     return h.hexdigest()[:16]
 
 
+def kernel_digest(path: str, prefix: bytes) -> str:
+    """sha256 of the bodies of every function whose symbol starts with
+    `prefix` (from its `sym:` label to its `.Lfunc_end` label), comments
+    skipped: a change elsewhere in the translation unit leaves it alone, so
+    a PMC row of one kernel stays valid across edits of the others."""
+    h = hashlib.sha256()
+    inside = False
+    with open(path, "rb") as f:
+        for line in f:
+            if not inside and line.startswith(prefix) and line.split(None, 1)[0].endswith(b":"):
+                inside = True
+            if inside:
+                if line.lstrip().startswith((b";", b"//")):
+                    continue
+                h.update(line)
+                if line.startswith(b".Lfunc_end"):
+                    inside = False
+    return h.hexdigest()[:16]
+
+
 step_isa, rollout_isa = sys.argv[1], sys.argv[2]
-info = f";step_isa={digest(step_isa)};policy_rollout_isa={digest(rollout_isa)}"
+info = (f";step_isa={digest(step_isa)};policy_rollout_isa={digest(rollout_isa)}"
+        f";step_kernel_isa={kernel_digest(step_isa, b'_ZN2dd11step_kernel')}"
+        f";rollout_kernel_isa={kernel_digest(step_isa, b'_ZN2dd14rollout_kernel')}")
 print('#include "dronestep.h"')
 print("#define DD_STR2(x) #x")
 print("#define DD_STR(x) DD_STR2(x)")

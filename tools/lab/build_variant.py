@@ -6,7 +6,12 @@ one source (each OLD must occur exactly once), compiles that source and links
 it with the product's other objects into _native/lab/lib_NAME.so.  The
 product sources stay free of lab switches.
 
-    python tools/lab/build_variant.py NAME FILE OLD NEW [OLD NEW ...]
+    python tools/lab/build_variant.py NAME FILE OLD NEW [OLD NEW ...] [-- FILE2 OLD NEW ...]
+
+Edits to several sources are groups separated by "--".  DD_VARIANT_UNITS
+(comma list, e.g. drone_step) limits the rebuilt translation units; the
+others are linked from the product build (a lab timing the step kernel need
+not wait for policy_rollout.hip).
 """
 import os
 import shutil
@@ -19,17 +24,29 @@ FLAGS = {"policy_mlp": ["-mllvm", "-disable-machine-licm"], "policy_rollout": ["
 
 
 def main():
-    name, fname, edits = sys.argv[1], sys.argv[2], sys.argv[3:]
+    name, rest = sys.argv[1], sys.argv[2:]
+    groups, cur = [], []
+    for a in rest:
+        if a == "--":
+            groups.append(cur)
+            cur = []
+        else:
+            cur.append(a)
+    groups.append(cur)
     src = f"/tmp/dd_variant_{name}"
     shutil.rmtree(src, ignore_errors=True)
     shutil.copytree(os.path.join(PKG, "csrc"), src)
-    path = os.path.join(src, fname)
-    text = open(path).read()
-    for old, new in zip(edits[::2], edits[1::2]):
-        if text.count(old) != 1:
-            raise SystemExit(f"{fname}: {old!r} occurs {text.count(old)} times")
-        text = text.replace(old, new)
-    open(path, "w").write(text)
+    fnames = []
+    for grp in groups:
+        fname, edits = grp[0], grp[1:]
+        fnames.append(fname)
+        path = os.path.join(src, fname)
+        text = open(path).read()
+        for old, new in zip(edits[::2], edits[1::2]):
+            if text.count(old) != 1:
+                raise SystemExit(f"{fname}: {old!r} occurs {text.count(old)} times")
+            text = text.replace(old, new)
+        open(path, "w").write(text)
     # the translation units the edit lands in (a header: every unit that includes it)
     def includes(f, seen=None):
         seen = seen if seen is not None else set()
@@ -41,7 +58,9 @@ def main():
                     includes(inc, seen)
         return seen
     units = [u for u in ("drone_step", "policy_mlp", "policy_rollout", "render")
-             if fname == u + ".hip" or fname in includes(u + ".hip")]
+             if any(f == u + ".hip" or f in includes(u + ".hip") for f in fnames)]
+    if os.environ.get("DD_VARIANT_UNITS"):
+        units = [u for u in units if u in os.environ["DD_VARIANT_UNITS"].split(",")]
     objs = []
     for u in ("drone_step", "policy_mlp", "policy_rollout", "render"):
         if u in units:
@@ -56,7 +75,7 @@ def main():
     out = os.path.join(PKG, "delivery_drone_amd", "_native", "lab", f"lib_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", out, *objs], check=True)
-    print(f"built {out} ({fname}: {len(edits) // 2} edit(s); rebuilt {units})")
+    print(f"built {out} ({', '.join(fnames)}; rebuilt {units})")
 
 
 if __name__ == "__main__":

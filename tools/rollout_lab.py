@@ -22,6 +22,8 @@ def main():
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--no-obs", action="store_true")
     p.add_argument("--philox", action="store_true", help="in-kernel Philox actions (config 5b) instead of a tensor")
+    p.add_argument("--warm", type=int, default=0, help="untimed back-to-back launches first (the DVFS steady state)")
+    p.add_argument("--burst", type=int, default=1, help="back-to-back launches per variant and round, each timed")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     cfg = EnvConfig(randomize_drone=True, auto_reset=True, seed=0)
@@ -43,16 +45,23 @@ def main():
             envs[v] = (e, [])
         torch.cuda.synchronize()
         names = list(envs)
+        for _ in range(args.warm):
+            for v in names:
+                envs[v][0].rollout(None if args.philox else acts, frames=args.frames, obs_out=obs, reward_out=rew,
+                                   done_out=done, write_obs=not args.no_obs)
+        torch.cuda.synchronize()
         for rnd in range(args.rounds):  # ABBA: alternate the order so position effects cancel
             for v in (names if rnd % 2 == 0 else names[::-1]):
                 e, ts = envs[v]
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                e.rollout(None if args.philox else acts, frames=args.frames, obs_out=obs, reward_out=rew,
-                          done_out=done, write_obs=not args.no_obs)
-                e1.record()
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(args.burst)]
+                for e0, e1 in evs:
+                    e0.record()
+                    e.rollout(None if args.philox else acts, frames=args.frames, obs_out=obs, reward_out=rew,
+                              done_out=done, write_obs=not args.no_obs)
+                    e1.record()
                 torch.cuda.synchronize()
-                ts.append(e0.elapsed_time(e1))
+                ts.extend(e0.elapsed_time(e1) for e0, e1 in evs)
         for v, (e, ts) in envs.items():
             med = statistics.median(ts)
             print(json.dumps({"envs": n, "frames": args.frames, "variant": v, "obs": not args.no_obs, "philox": args.philox,
