@@ -104,7 +104,9 @@ def test_policy_rollout_notebook_reward_and_timeout(mode, compute, gpu_device):
                          (r_obs, r_acts, r_lp, r_rew, r_done, r_erew, r_edone)):
         assert torch.equal(got, want)
     if mode == "notebook":
-        assert torch.equal(fused.shaped_hist, ref.shaped_hist)
+        # bit patterns: a lane re-spawned in the last frames still holds the
+        # history's NaN ("prev_state None"), which torch.equal never equates
+        assert torch.equal(fused.shaped_hist.view(torch.int64), ref.shaped_hist.view(torch.int64))
     assert_same_state(fused, ref)
     assert bool((ref.steps >= 0).all()) and bool(done.any())
     assert bool((rew < -400).any())  # max_steps timeouts (-500) happened inside the launch
