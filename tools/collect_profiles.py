@@ -60,11 +60,12 @@ def main():
             info = lines[0].split("build_info:", 1)[1].split(";md5")[0].split("; md5")[0].strip()
         with open(os.path.join(dst, "pytest_gpu_tail.txt"), "w") as f:
             f.write("\n".join(lines[:1] + lines[-3:]) + "\n")
-    for name in ("c3", "16m", "extra", "c5"):
+    for name in ("c3", "16m", "extra", "c5", "k20"):
         hits = glob.glob(os.path.join(src, f"prof_{name}", "*kernel_stats.csv"))
         if hits:
             shutil.copy(hits[0], os.path.join(dst, f"rocprof_kernel_stats_{name}.csv"))
-    for pat in ("bench_*.json", "prof_*_bench.json", "smoke.log"):
+    for pat in ("bench_*.json", "prof_*_bench.json", "smoke.log", "*.jsonl", "*trace_summary.json",
+                "*summary.json"):
         for f in glob.glob(os.path.join(src, pat)):
             shutil.copy(f, dst)
     rows = {}
