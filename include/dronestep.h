@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define DD_ABI_VERSION 11 /* 11: shaped_mode (REINFORCE reward), DDRolloutIO.kernel, dd_rollout_kernel,
+#define DD_ABI_VERSION 12 /* 12: spawns drawn from Philox4x32-7; 11: shaped_mode (REINFORCE reward), DDRolloutIO.kernel, dd_rollout_kernel,
                               dd_device_errors; 10: DDStepIO.state_out (ping-pong state) */
 
 /* Storage precision of the SoA floating-point fields. */
@@ -151,7 +151,7 @@ typedef struct DDConfig {
                                    re-spawned and returns its reset observation
                                    with reward 0 and done 0 (next-step reset). */
     int32_t _pad;
-    uint64_t seed; /* Philox4x32-10 key for spawn draws */
+    uint64_t seed; /* key of the spawn draws: Philox4x32-7 of (env id, episode) (ABI 12; 10 rounds before) */
 } DDConfig;
 
 /* The SoA.  Every pointer addresses N elements in device memory.  The ten

@@ -478,13 +478,47 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
     // infinite x fails the test, as the reference's comparisons fail)
     const bool near_pad = upright && fma(-fabs(s.x), 0x1p-30, fabs(s.x - s.px)) <= rx + 1.0 &&
                           fma(-fabs(s.y), 0x1p-30, fabs(s.y - s.py)) <= ry + 1.0;
-    if (near_pad) {
+    if constexpr (kRef && !kExact) {
+        // The fast frame, reference world: one branch, taken by the lanes that
+        // are near the pad AND slow.  The speed's edge band is tested on every
+        // lane (two VALU) rather than inside a branch of its own.
+        const bool edge = fabs(ss - 9.0) <= 0x1p-20;
+        static_assert(reference_config().max_landing_velocity == 3.0, "the squared speed limit");
+        const bool slow = kDefer ? !(ss > 9.0) : !(s.speed > c.max_landing_velocity);
+        risky |= near_pad & edge;
+        // kFlat (the loops' frame, one wave per SIMD): no branch at all — every
+        // lane forms the bottom centre and the tests are masked (config 5,
+        // 65,536 x 256: -3.4 %, profiles/r06/lab/rollout_bounds.jsonl
+        // `flatpad`); the step kernel (four waves per SIMD) keeps the branch
+        const bool pad_test = near_pad & slow;
+        if (kFlat || pad_test) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
+            // upright (|angle| <= 20): the small-angle sin / cos, within 3e-13
+            // (trig.h); bx, by then lie within 1e-11 of the reference's, far
+            // inside the risky band below
+            static_assert(reference_config().max_landing_angle == 20.0 &&
+                              reference_config().drone_half_height == 10.0 &&
+                              reference_config().platform_half_width == 50.0 &&
+                              reference_config().platform_half_height == 10.0,
+                          "sincos_upright_deg's range; the pad's half extents");
+            double sb, cb;
+            trig::sincos_upright_deg<kSgpr>(s.angle, &sb, &cb);
+            const double bx = s.x - c.drone_half_height * sb;
+            const double by = s.y + c.drone_half_height * cb;
+            // px - 50 <= bx <= px + 50 as |bx - px| <= 50 (likewise y): the two
+            // forms can only disagree where bx lies within a few ulps of an
+            // edge, and such a lane is inside the risky band (2^-19 relative,
+            // as before) and redone with the reference's own comparisons
+            const double dxp = bx - s.px, dyp = by - s.py;
+            on_pad = pad_test & (fabs(dxp) <= c.platform_half_width) & (fabs(dyp) <= c.platform_half_height);
+            const double m = fmin(fabs(fabs(dxp) - c.platform_half_width), fabs(fabs(dyp) - c.platform_half_height));
+            risky |= pad_test & (m <= 0x1p-19 * (1.0 + fabs(bx) + fabs(by)));
+        }
+    } else if (near_pad) {
         // (lanes out of this reach of the pad: on_pad = false exactly as the
         // reference's comparisons give, the bottom centre lying within
         // |half_height| (+ rounding) of (x, y); NaN fails both tests alike)
         const bool edge = kRef ? fabs(ss - 9.0) <= 0x1p-20 : close(s.speed, c.max_landing_velocity);
-        static_assert(reference_config().max_landing_velocity == 3.0, "kDefer's squared speed limit");
-        bool slow = kDefer ? !(ss > 9.0) : !(s.speed > c.max_landing_velocity);
+        bool slow = !(s.speed > c.max_landing_velocity);
         if constexpr (kExact) {
             if (edge) {  // the reference's speed: sqrt(pow(vx, 2) + pow(vy, 2))
                 double sq = 0.0, v = s.vx;
@@ -499,21 +533,10 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
             risky |= edge;
         }
         if (slow) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
-            double sb, cb, bx, by;
-            if constexpr (kRef && !kExact) {
-                // upright (|angle| <= 20): the small-angle sin / cos, within
-                // 3e-13 (trig.h); bx, by then lie within 1e-11 of the
-                // reference's, far inside the risky band below
-                static_assert(reference_config().max_landing_angle == 20.0 &&
-                              reference_config().drone_half_height == 10.0, "sincos_upright_deg's range");
-                trig::sincos_upright_deg<kSgpr>(s.angle, &sb, &cb);
-                bx = s.x - c.drone_half_height * sb;
-                by = s.y + c.drone_half_height * cb;
-            } else {
-                sincos_deg<kExact, kSgpr>(s.angle, &sb, &cb);
-                bx = s.x + (0.0 * cb - c.drone_half_height * sb);
-                by = s.y + (0.0 * sb + c.drone_half_height * cb);
-            }
+            double sb, cb;
+            sincos_deg<kExact, kSgpr>(s.angle, &sb, &cb);
+            const double bx = s.x + (0.0 * cb - c.drone_half_height * sb);
+            const double by = s.y + (0.0 * sb + c.drone_half_height * cb);
             on_pad = (s.px - c.platform_half_width <= bx) & (bx <= s.px + c.platform_half_width) &
                      (s.py - c.platform_half_height <= by) & (by <= s.py + c.platform_half_height);
             if constexpr (!kExact) {
