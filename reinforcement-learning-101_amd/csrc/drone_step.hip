@@ -775,7 +775,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
         double reward;
         const bool was_done = (s.status & DD_ST_DONE) != 0;
         auto fast = [&]() __attribute__((always_inline)) {
-            return frame_checked<kRef, true, kSplit, true>(k, sw, act, s, &tt);  // kSplit: the writer finishes it
+            return frame_checked<kRef, true, kSplit, true, T>(k, sw, act, s, &tt);  // kSplit: the writer finishes it
         };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the
@@ -787,6 +787,8 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
                     if constexpr (kAhead) ahead.respawn(sw, k.c.max_fuel, env, s);
                     else spawn(sw, k.c.max_fuel, env, s);
                     reward = 0.0;
+                    tt.s = 0.0;  // sin / cos of the spawn angle 0, as next_trig gives them
+                    tt.c = 1.0;
                 }
             }
         } else if (was_done) {  // sticky done (game_engine.py:107-111)
@@ -854,7 +856,6 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
         if constexpr (kObs && !kSplit) observe<kGuard>(k, s, tile[kHeld ? (f & 1) : 0] + roff);
         // the obs above sees the unrounded frame, like dd_step's
         quantize<T, kRef>(s);
-        next_trig(s, tt);  // frame f + 1's thrust rotation, beside the rest of this frame
         if constexpr (kObs && !kSplit) {
             if constexpr (kHeld) {
                 store_held_wave(held, rsrc_over(obs_prev, prev_bytes));  // frame f - 1's rows

@@ -486,12 +486,15 @@ __device__ __forceinline__ double frame(const Consts& k, const DDConfig& sw, uin
         static_assert(reference_config().max_landing_velocity == 3.0, "the squared speed limit");
         const bool slow = kDefer ? !(ss > 9.0) : !(s.speed > c.max_landing_velocity);
         risky |= near_pad & edge;
-        // kFlat (the loops' frame, one wave per SIMD): no branch at all — every
-        // lane forms the bottom centre and the tests are masked (config 5,
-        // 65,536 x 256: -3.4 %, profiles/r06/lab/rollout_bounds.jsonl
-        // `flatpad`); the step kernel (four waves per SIMD) keeps the branch
+        // Where the branch pays depends on the kernel (profiles/r06/lab/
+        // rollout_nearpad_respawn_variants.jsonl, rollout_trigearly.jsonl):
+        // the step kernel and the split rollout's frame waves (kDefer) keep it
+        // (config 5: 0.2252 / 0.2120 ms with it against 0.2300 / 0.2165
+        // without); the single-role loops (kFlat, not kDefer: 262,144 x 256,
+        // and the fused policy rollout) form the bottom centre on every lane
+        // and mask the tests (0.8548 against 0.8751 ms)
         const bool pad_test = near_pad & slow;
-        if (kFlat || pad_test) {  // get_bottom_center: rotate_point(0, height / 2, angle) on the updated angle
+        if ((kFlat && !kDefer) || pad_test) {  // get_bottom_center: rotate_point(0, height / 2, angle), updated angle
             // upright (|angle| <= 20): the small-angle sin / cos, within 3e-13
             // (trig.h); bx, by then lie within 1e-11 of the reference's, far
             // inside the risky band below
@@ -623,12 +626,18 @@ __device__ __forceinline__ double finish_deferred(Lane& s, bool was_done, bool a
 // from the kept state with glibc's functions (a wave-uniform rare branch; as
 // an out-of-line call, or through an LDS slot, it measured slower or equal,
 // DESIGN.md §3.2).
-template <bool kRef, bool kFlat, bool kDefer = false, bool kPipe = false>
+// kPipe: *tt holds the sin / cos of the frame's starting angle and receives
+// those of the next frame's, i.e. of this frame's angle rounded to the
+// storage width TQ.  Taken before the redo's branch, beside the frame's flag
+// tests: the angle update has no transcendental, so the exact redo ends on
+// the same angle.  (A re-spawn after the frame resets it to (+0, 1).)
+template <bool kRef, bool kFlat, bool kDefer = false, bool kPipe = false, typename TQ = double>
 __device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s,
-                                                const ThrustTrig* tt = nullptr) {
+                                                ThrustTrig* tt = nullptr) {
     const Lane s0 = s;
     bool risky = false;
     double reward = frame<kRef, kFlat, false, kDefer, kPipe>(k, sw, act, s, &risky, tt);
+    if constexpr (kPipe) sincos_deg<false>((double)(TQ)s.angle, &tt->s, &tt->c);
     if (__builtin_expect(__ballot(risky) != 0, 0)) {
         if (risky) {
             s = s0;

@@ -22,7 +22,7 @@ __all__ = [
     "NativeLibraryError",
 ]
 
-DD_ABI_VERSION = 11
+DD_ABI_VERSION = 12
 DD_F32, DD_F64 = 0, 1
 DD_ACT_BITMASK, DD_ACT_F32X3, DD_ACT_U8X3, DD_ACT_PHILOX = 0, 1, 2, 3
 DD_ST_DONE, DD_ST_LANDED, DD_ST_CRASHED, DD_ST_PLAT_LEFT = 1, 2, 4, 8
@@ -180,8 +180,10 @@ def library_path() -> str:
     return os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "libdronestep.so")
 
 
-def load(path: str) -> ctypes.CDLL:
-    """Load a build of the library at ``path`` and bind the header's signatures."""
+def load(path: str, *, abi_versions=None) -> ctypes.CDLL:
+    """Load a build of the library at ``path`` and bind the header's signatures.
+    ``abi_versions``: the versions accepted (default: this header's only); A/B
+    labs pass the two sides of a version bump whose signatures are unchanged."""
     if not os.path.exists(path):
         raise NativeLibraryError(
             f"HIP extension not built: {path} is missing. "
@@ -196,7 +198,7 @@ def load(path: str) -> ctypes.CDLL:
         fn = getattr(handle, name)
         fn.restype = restype
         fn.argtypes = argtypes
-    if handle.dd_abi_version() != DD_ABI_VERSION:
+    if handle.dd_abi_version() not in (abi_versions or (DD_ABI_VERSION,)):
         raise NativeLibraryError(f"{path}: ABI version mismatch; rebuild it")
     return handle
 

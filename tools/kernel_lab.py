@@ -41,7 +41,7 @@ def main():
                    help="one env per variant (default: every variant steps the same buffers)")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
-    libs = {v: abi.load(os.path.join(LAB, f"lib_{v}.so")) for v in args.variants.split(",")}
+    libs = {v: abi.load(os.path.join(LAB, f"lib_{v}.so"), abi_versions=(11, 12)) for v in args.variants.split(",")}
     cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=0)
     G = args.graph_steps
     for n in [int(x) for x in args.envs.split(",")]:

@@ -26,7 +26,7 @@ LAB = os.path.join(REPO, "reinforcement-learning-101_amd", "delivery_drone_amd",
 def run(lib, n, frames, auto, philox, start, acts, dev):
     cfg = EnvConfig(randomize_drone=True, auto_reset=auto, seed=3)
     e = VecDroneEnv(n, device=dev, config=cfg)
-    e._lib = abi.load(os.path.join(LAB, f"lib_{lib}.so"))
+    e._lib = abi.load(os.path.join(LAB, f"lib_{lib}.so"), abi_versions=(11, 12))
     e.load_state_dict(start)
     obs = torch.full((frames, n, 15), float("nan"), device=dev)
     rew = torch.empty(frames, n, device=dev)
@@ -40,7 +40,7 @@ def run(lib, n, frames, auto, philox, start, acts, dev):
 def run_steps(lib, n, frames, precision, start, acts, dev):
     cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=5)
     e = VecDroneEnv(n, device=dev, config=cfg, precision=precision)
-    e._lib = abi.load(os.path.join(LAB, f"lib_{lib}.so"))
+    e._lib = abi.load(os.path.join(LAB, f"lib_{lib}.so"), abi_versions=(11, 12))
     e.load_state_dict(start)
     outs = []
     for t in range(frames):

@@ -39,7 +39,7 @@ def main():
             # every variant steps the same buffers (physical placement out of the A/B)
             e = VecDroneEnv.__new__(VecDroneEnv)
             e.__dict__.update(shared.__dict__)
-            e._lib = abi.load(os.path.join(LAB, f"lib_{v}.so"))
+            e._lib = abi.load(os.path.join(LAB, f"lib_{v}.so"), abi_versions=(11, 12))
             e.rollout(None if args.philox else acts, frames=args.frames, obs_out=obs, reward_out=rew, done_out=done,
                       write_obs=not args.no_obs)
             envs[v] = (e, [])
