@@ -617,8 +617,6 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
     __shared__ __attribute__((aligned(16))) f32x4 stage[kSplit ? kBlock / kWave : 1][2][kSplit ? kStageQ : 1]
                                                       [kSplit ? kWave : 1];
     __shared__ int ctr[2][kBlock / kWave];  // kSplit: produced, consumed
-    // kSplit: each frame lane's starting state, for the rare exact redo (frame_checked kSlot)
-    __shared__ __attribute__((aligned(16))) T keep[kSplit ? kBlock / kWave : 1][kSplit ? 9 : 1][kSplit ? kWave : 1];
     if constexpr (kSplit) {
         if (threadIdx.x < 2 * (kBlock / kWave)) ctr[threadIdx.x >> 2][threadIdx.x & 3] = 0;
         __syncthreads();
@@ -777,9 +775,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock, kRollMinWaves) void r
         double reward;
         const bool was_done = (s.status & DD_ST_DONE) != 0;
         auto fast = [&]() __attribute__((always_inline)) {
-            // kSplit: the writer finishes it
-            return frame_checked<kRef, true, kSplit, true, T, kSplit>(
-                k, sw, act, s, &tt, &keep[kSplit ? threadIdx.x / kWave : 0][0][kSplit ? threadIdx.x & (kWave - 1) : 0]);
+            return frame_checked<kRef, true, kSplit, true, T>(k, sw, act, s, &tt);  // kSplit: the writer finishes it
         };
         if constexpr (kAuto) {
             // next-step reset, fixed up after the frame: every lane runs the

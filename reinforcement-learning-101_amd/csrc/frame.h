@@ -634,38 +634,16 @@ __device__ __forceinline__ double finish_deferred(Lane& s, bool was_done, bool a
 // storage width TQ.  Taken before the redo's branch, beside the frame's flag
 // tests: the angle update has no transcendental, so the exact redo ends on
 // the same angle.  (A re-spawn after the frame resets it to (+0, 1).)
-// kSlot (the split rollout's frame waves, kDefer): the frame's starting state
-// is kept in the lane's LDS slot `slot` (its fields at the storage width TQ,
-// which holds them exactly, one word apart per lane: slot[j * 64]) instead of
-// in registers for the whole frame; only a risky lane reads it back.  In the
-// frame wave the state the frame leaves alone (px, py, total under kDefer,
-// episode) is taken from the lane as it stands.
-template <bool kRef, bool kFlat, bool kDefer = false, bool kPipe = false, typename TQ = double, bool kSlot = false>
+template <bool kRef, bool kFlat, bool kDefer = false, bool kPipe = false, typename TQ = double>
 __device__ __forceinline__ double frame_checked(const Consts& k, const DDConfig& sw, uint32_t act, Lane& s,
-                                                ThrustTrig* tt = nullptr, TQ* slot = nullptr) {
-    static_assert(!kSlot || (kDefer && kRef), "the LDS slot keeps the deferred frame's fields only");
-    Lane s0;
-    if constexpr (kSlot) {
-        slot[0 * 64] = (TQ)s.x; slot[1 * 64] = (TQ)s.y; slot[2 * 64] = (TQ)s.vx; slot[3 * 64] = (TQ)s.vy;
-        slot[4 * 64] = (TQ)s.angle; slot[5 * 64] = (TQ)s.omega; slot[6 * 64] = (TQ)s.fuel;
-        *reinterpret_cast<uint32_t*>(slot + 7 * 64) = s.status;
-        *reinterpret_cast<int32_t*>(slot + 8 * 64) = s.steps;
-    } else {
-        s0 = s;
-    }
+                                                ThrustTrig* tt = nullptr) {
+    const Lane s0 = s;  // (in an LDS slot instead: config 5 0.215 -> 0.226 ms, profiles/r06/lab/rollout_s0lds.jsonl)
     bool risky = false;
     double reward = frame<kRef, kFlat, false, kDefer, kPipe>(k, sw, act, s, &risky, tt);
     if constexpr (kPipe) sincos_deg<false>((double)(TQ)s.angle, &tt->s, &tt->c);
     if (__builtin_expect(__ballot(risky) != 0, 0)) {
         if (risky) {
-            if constexpr (kSlot) {
-                s.x = slot[0 * 64]; s.y = slot[1 * 64]; s.vx = slot[2 * 64]; s.vy = slot[3 * 64];
-                s.angle = slot[4 * 64]; s.omega = slot[5 * 64]; s.fuel = slot[6 * 64];
-                s.status = *reinterpret_cast<uint32_t*>(slot + 7 * 64);
-                s.steps = *reinterpret_cast<int32_t*>(slot + 8 * 64);
-            } else {
-                s = s0;
-            }
+            s = s0;
             reward = frame<kRef, false, true>(k, sw, act, s, nullptr);
         }
     }
