@@ -349,6 +349,13 @@ __device__ __forceinline__ void load_image(const float* __restrict__ packed, f32
         // which waits vmcnt(0) at the first use of an ordinary load left
         // outstanding beside an LDS-DMA, does not track them: the vmcnt
         // below covers them (they are older than every piece).
+        // CAUTION: gfx9 has no interlock on a VMEM result, and the
+        // compiler does not know these registers are pending until that
+        // hand-written s_waitcnt; a codegen that copied, spilled or
+        // rematerialised xa / xb before it would read stale data.  Any change
+        // of compiler (or of this prologue) must re-run the GPU tests
+        // test_observations_at_any_offset and test_actor_probs_match_notebook_model
+        // (tests/test_gpu_policy.py), which catch exactly that.
         const int64_t d = tile * kCols + (lane & 31);
         const float* rp = p.obs + (d < p.n ? d : 0) * kIn + 7 * h;
         asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:16"

@@ -293,3 +293,33 @@ def test_layernorm_parameters_at_the_edges(gpu_device, compute, ln):
         scale = float(want.abs().max()) + 1.0
         close(got.cpu().numpy(), want.cpu().numpy(), 1e-4 if k == 1 else 0.0,
               (1e-5 if k == 3 else 1e-4) * (scale if k == 1 else 1.0))
+
+
+@pytest.mark.parametrize("compute", COMPUTE)
+def test_confident_actor_tail_vs_torch_fp32(gpu_device, compute):
+    """the Sigmoid is v_rcp(1 + v_exp(-z log2 e)), whose relative
+    error grows with |z| (about |z| f32 ulps of p for z < 0).  A network whose
+    logits sit near -14, -8 and +4 (probabilities ~8e-7, ~3e-4, ~1 - 0.018):
+    probabilities against torch fp32 to a RELATIVE bound (f32 5e-5, f16x3 5e-4:
+    it covers the logits' own difference from torch's summation order, dp/p =
+    dz, plus the exp's ~|z| ulps), and the summed log-probability of sampled
+    actions to 5e-5 (5e-4) x (1 + |lp|)."""
+    torch.manual_seed(11)
+    sd = _random_sd(3)
+    sd["9.bias"] = torch.tensor([-14.0, -8.0, 4.0])
+    sd["9.weight"] = sd["9.weight"] * 0.05  # logits dominated by the bias: deep in the tails
+    ref = gd.torch_mlp({k: v.numpy() for k, v in sd.items()}, device=gpu_device)
+    net = MlpNet(sd, device=gpu_device, compute=compute)
+    obs = torch.randn(4096, 15, device=gpu_device)
+    with torch.no_grad():
+        want = ref(obs).double()
+    got = net(obs).double()
+    rel = 5e-5 if compute == "f32" else 5e-4
+    assert float(want[:, 0].max()) < 1e-5 and float(want[:, 2].min()) > 0.95  # the tails are exercised
+    err = ((got - want).abs() / want.clamp_min(1e-30))
+    err[:, 2] = (got[:, 2] - want[:, 2]).abs() / (1 - want[:, 2]).clamp_min(1e-30)  # p ~ 1: relative in 1 - p
+    assert float(err.max()) <= rel, f"max relative error {float(err.max()):.3g}"
+    actions, lp, probs = net.act(obs, seed=3, step=1, probs=True)
+    bits = torch.stack([(actions.long() >> j) & 1 for j in range(3)], 1).double()
+    want_lp = Bernoulli(probs=want).log_prob(bits).sum(1)
+    assert float(((lp.double() - want_lp).abs() / (1 + want_lp.abs())).max()) <= rel
