@@ -56,8 +56,6 @@ def _actor(dev):
 @pytest.mark.parametrize("cfg_name", sorted(CONFIGS))
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_flags_exact_near_every_boundary(precision, cfg_name, path, gpu_device):
-    if path == "policy" and precision == "f64":
-        pytest.skip("dd_policy_rollout: f32 storage is the notebooks' layout; f64 is covered by step / rollout")
     cfg = EnvConfig(**CONFIGS[cfg_name])
     seed = {"f64": 11, "f32": 12}[precision] + (100 if cfg_name != "ref" else 0)
     st, acts, fam, dist = ts.generate(N, precision, seed=seed, config=cfg)
