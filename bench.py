@@ -212,82 +212,40 @@ def cpu_baseline(seconds: float, workers: int, seed: int, share: dict | None = N
 
 
 # ------------------------------------------------------------------- GPU bench
-class KernelSpanEvents:
-    """Two HIP timing events recorded by EVENT-RECORD NODES inside the timed
-    hipGraphs: after capture (torch.cuda.CUDAGraph(keep_graph=True)) a node
-    recording `head` is added before the graph's root nodes and one recording
-    `tail` after its leaves (hipGraphAddEventRecordNode /
-    hipGraphAddDependencies on raw_cuda_graph()), then the graph is
-    instantiated.  Recorded in the first and the last timed graph they bracket
-    the step kernels only; the host's graph submission before the first kernel
-    is outside.  torch refuses external events on ROCm, so the
-    HIP runtime torch itself loaded is called through ctypes."""
+class KernelSpanStamps:
+    """GPU wall-clock stamps around the timed step kernels.  A one-lane kernel
+    (dd_stamp, s_memrealtime at the GPU's constant wall-clock rate) is
+    captured at the head of the first timed hipGraph and one at the tail of
+    the last, so the stamps bracket the K step kernels and not the host's
+    graph submission before the first one.  They replaced
+    event-record nodes added to the graph after capture: a graph holding
+    those launched ~50 us slower from the host at K = 20 and the wall clock
+    paid for it (tools/lab/launch_probe.py, profiles/r06/lab/).  Slots 2 and
+    3 are for the calibration graph of the two stamps alone."""
 
-    def __init__(self):
+    def __init__(self, lib, dev):
         import ctypes
         import torch
-        torch.cuda.init()
-        path = None
-        with open("/proc/self/maps") as f:
-            for line in f:
-                if "libamdhip64.so" in line:
-                    path = line.split()[-1]
-                    break
-        if path is None:
-            raise RuntimeError("libamdhip64.so is not mapped in this process")
-        self.path = path
-        self.hip = ctypes.CDLL(path)
-        self.c = ctypes
-        self.head, self.tail = ctypes.c_void_p(), ctypes.c_void_p()
-        for ev in (self.head, self.tail):
-            self._check(self.hip.hipEventCreate(ctypes.byref(ev)), "hipEventCreate")
+        self.c, self.lib = ctypes, lib
+        self.slots = torch.zeros(4, dtype=torch.int64, device=dev)
+        khz = ctypes.c_int(0)
+        rc = lib.dd_wall_clock_khz(ctypes.byref(khz))
+        if rc != 0 or khz.value <= 0:
+            raise RuntimeError(f"dd_wall_clock_khz failed: rc {rc}, {khz.value} kHz")
+        self.khz = khz.value
 
-    def _check(self, rc, what):
+    def stamp(self, slot: int, stream) -> None:
+        """Launch the stamp kernel for `slot` on `stream` (captured when the stream is capturing)."""
+        rc = self.lib.dd_stamp(self.c.c_void_p(self.slots.data_ptr() + 8 * slot), self.c.c_void_p(stream.cuda_stream))
         if rc != 0:
-            raise RuntimeError(f"{what} failed: hipError {rc}")
+            raise RuntimeError(f"dd_stamp failed: rc {rc}")
 
-    def _nodes(self, fn, *lead):
-        c = self.c
-        n = c.c_size_t(0)
-        self._check(fn(*lead, None, c.byref(n)), fn.__name__)
-        arr = (c.c_void_p * max(1, n.value))()
-        self._check(fn(*lead, arr, c.byref(n)), fn.__name__)
-        return [c.c_void_p(arr[i]) for i in range(n.value)]
-
-    def add_nodes(self, graph, head: bool, tail: bool) -> None:
-        """Event-record nodes into a captured, not yet instantiated graph."""
-        c, hip = self.c, self.hip
-        g = c.c_void_p(graph.raw_cuda_graph())
-        if tail:
-            leaves = [nd for nd in self._nodes(hip.hipGraphGetNodes, g)
-                      if not self._nodes(hip.hipGraphNodeGetDependentNodes, nd)]
-            deps = (c.c_void_p * len(leaves))(*[nd.value for nd in leaves])
-            node = c.c_void_p()
-            self._check(hip.hipGraphAddEventRecordNode(c.byref(node), g, deps, c.c_size_t(len(leaves)), self.tail),
-                        "hipGraphAddEventRecordNode(tail)")
-        if head:
-            roots = self._nodes(hip.hipGraphGetRootNodes, g)
-            node = c.c_void_p()
-            self._check(hip.hipGraphAddEventRecordNode(c.byref(node), g, None, c.c_size_t(0), self.head),
-                        "hipGraphAddEventRecordNode(head)")
-            for r in roots:
-                self._check(hip.hipGraphAddDependencies(g, c.byref(node), c.byref(r), c.c_size_t(1)),
-                            "hipGraphAddDependencies")
-
-    def record(self, which: str, stream) -> None:
-        """An ordinary record on the stream (the eager path)."""
-        ev = self.head if which == "head" else self.tail
-        self._check(self.hip.hipEventRecord(ev, self.c.c_void_p(stream.cuda_stream)), "hipEventRecord")
-
-    def elapsed_ms(self) -> float:
-        ms = self.c.c_float(0.0)
-        self._check(self.hip.hipEventSynchronize(self.tail), "hipEventSynchronize")
-        self._check(self.hip.hipEventElapsedTime(self.c.byref(ms), self.head, self.tail), "hipEventElapsedTime")
-        return float(ms.value)
-
-    def close(self):
-        for ev in (self.head, self.tail):
-            self.hip.hipEventDestroy(ev)
+    def elapsed_ms(self, first: int = 0, last: int = 1) -> float:
+        """Milliseconds between two stamps (synchronises the device)."""
+        import torch
+        torch.cuda.synchronize(self.slots.device)
+        v = self.slots.cpu().tolist()
+        return (v[last] - v[first]) / self.khz
 
 
 def time_steps(env, rows, steps, graph_steps, stream, write_obs=True):
@@ -1012,26 +970,28 @@ def main():
     # K = 20, W = 5: four 5-launch replays leave gaps, profiles/r02/k20.)
     G = min(args.graph_steps, max(args.steps, 1))
     graphs = {}
-    # The kernels' own span: timing events recorded as event nodes INSIDE the
-    # timed graphs (KernelSpanEvents), one at the head of the first graph of
-    # the timed region and one at the tail of its last.  They bracket the K
-    # step kernels only, not the host's graph submission before the first
-    # one (at K = 20 that submission gap sat inside the stream events below
-    # and priced launch overhead into roofline.frac: VERDICT r05 #1).
-    spans = KernelSpanEvents()
+    # The kernels' own span: GPU wall-clock stamps written by one-lane kernels
+    # captured INSIDE the timed graphs (KernelSpanStamps), one at the head of
+    # the first graph of the timed region and one at the tail of its last.
+    # They bracket the K step kernels only, not the host's graph submission
+    # before the first one (at K = 20 that submission gap sat inside the
+    # stream events below and priced launch overhead into roofline.frac:
+    # VERDICT r05 #1).
+    spans = KernelSpanStamps(env._lib, dev)
     seq = ([G] * (args.steps // G) + ([args.steps % G] if args.steps % G else [])) if G > 0 else []
     timed = [(k, j == 0, j == len(seq) - 1) for j, k in enumerate(seq)]
 
     def graph_of(k: int, head: bool = False, tail: bool = False):
         key = (k, head, tail)
         if key not in graphs:
-            g = torch.cuda.CUDAGraph(keep_graph=head or tail)
+            g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=stream):
+                if head:
+                    spans.stamp(0, stream)
                 for i in range(k):
                     env.step(rows[i % args.action_rows], write_obs=write_obs)
-            if head or tail:
-                spans.add_nodes(g, head, tail)
-                g.instantiate()
+                if tail:
+                    spans.stamp(1, stream)
             graphs[key] = g
         return graphs[key]
 
@@ -1057,10 +1017,10 @@ def main():
 
         def run_timed():
             if G <= 0:
-                spans.record("head", stream)
+                spans.stamp(0, stream)
                 for _ in range(args.steps):
                     one_step()
-                spans.record("tail", stream)
+                spans.stamp(1, stream)
                 return
             for key in timed:
                 graphs[key].replay()
@@ -1082,30 +1042,22 @@ def main():
             torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    span_ms = spans.elapsed_ms()
-    spans.close()
-    # The event-record nodes cost a fixed ~10 us per head/tail pair on top of
-    # the kernels (tools/lab/graph_event_probe.py: span = 10.5 us + N x 7.9 us
-    # over N = 1..40 kernels, and a graph holding only the two nodes spans the
-    # same 10.5 us).  So an untimed graph of the two nodes alone, replayed
-    # after the timed region, measures that overhead and it is subtracted.
+    span_ms = spans.elapsed_ms(0, 1)
+    # The stamps' own cost (the head stamp's kernel end and the tail stamp's
+    # dispatch lie inside the span): an untimed graph of the two stamps
+    # alone, replayed after the timed region, measures it and it is
+    # subtracted.
     marker_ms = 0.0
     if G > 0:
         import statistics
-        import warnings
-        cal = KernelSpanEvents()
-        gc = torch.cuda.CUDAGraph(keep_graph=True)
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore")  # "The CUDA Graph is empty": it holds only the two event nodes
-            with torch.cuda.graph(gc, stream=stream):
-                pass
-        cal.add_nodes(gc, True, True)
-        gc.instantiate()
+        gc = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream), torch.cuda.graph(gc, stream=stream):
+            spans.stamp(2, stream)
+            spans.stamp(3, stream)
         cals = []
         for _ in range(7):
             gc.replay()
-            cals.append(cal.elapsed_ms())
-        cal.close()
+            cals.append(spans.elapsed_ms(2, 3))
         marker_ms = statistics.median(cals)
     kernel_ms = span_ms - marker_ms
 
@@ -1162,9 +1114,10 @@ def main():
             "bytes_per_env": bytes_env,
             "kernel": f"dd::step_kernel<{'float' if args.precision == 'f32' else 'double'}, 0, true, 0>",
             "us_per_launch": round(step_ms * 1e3, 4),
-            "timing": ("HIP timing events recorded as nodes inside the timed hipGraphs, at the head of the first "
-                       "and the tail of the last: (their span - the span of a graph of the two nodes alone) / K, "
-                       "the K step kernels' own time (the host's graph submission excluded; max over ranks)"),
+            "timing": ("GPU wall-clock stamps (dd_stamp: one-lane kernels, s_memrealtime) captured inside the timed "
+                       "hipGraphs, at the head of the first and the tail of the last: (their span - the span of a "
+                       "graph of the two stamps alone) / K, the K step kernels' own time (the host's graph "
+                       "submission excluded; max over ranks)"),
             "span_us": round(span_ms * 1e3, 2),
             "marker_overhead_us": round(marker_ms * 1e3, 2),
             "stream_events": {"us_per_launch": round(gpu_ms / args.steps * 1e3, 4),

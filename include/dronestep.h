@@ -447,6 +447,14 @@ const char *dd_build_info(void);
  * any bit to *mismatches (device memory). */
 int dd_selftest_sqrt(uint64_t seed, int64_t n, unsigned long long *mismatches, void *stream);
 
+/* Measurement helpers for bench.py (not reference interfaces).  dd_stamp
+ * launches a one-lane kernel on `stream` that writes the GPU's constant-rate
+ * wall clock to *slot (device memory) when it runs; captured into a hipGraph
+ * between step launches it stamps that point of the graph.  dd_wall_clock_khz
+ * gives the clock's rate (hipDeviceAttributeWallClockRate, current device). */
+int dd_stamp(unsigned long long *slot, void *stream);
+int dd_wall_clock_khz(int *khz);
+
 #ifdef __cplusplus
 }
 #endif

@@ -945,6 +945,14 @@ __global__ __launch_bounds__(kBlock) void sqrt_selftest_kernel(uint64_t seed, ui
     }
 }
 
+// dd_stamp kernel: one lane stores the GPU's constant-rate wall clock
+// (s_memrealtime) with a vector store.  Captured into a hipGraph beside the
+// step kernels it marks where the graph reaches that point (bench.py).
+__global__ __launch_bounds__(kWave) void stamp_kernel(unsigned long long* slot) {
+    const unsigned long long t = (unsigned long long)wall_clock64();
+    if (threadIdx.x == 0) *slot = t;
+}
+
 // dd_shaped_reset kernel: the notebook reward's history restarts from the
 // current state (slot 0 = its distance, slot 1 = none).
 template <typename T>
@@ -1502,6 +1510,20 @@ int dd_selftest_sqrt(uint64_t seed, int64_t n, unsigned long long* mismatches, v
                            (uint64_t)first, len, mismatches);
     }
     return dd::finish();
+}
+
+int dd_stamp(unsigned long long* slot, void* stream) {
+    if (!slot) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dd::stamp_kernel, dim3(1), dim3(dd::kWave), 0, static_cast<hipStream_t>(stream), slot);
+    return dd::finish();
+}
+
+int dd_wall_clock_khz(int* khz) {
+    if (!khz) return hipErrorInvalidValue;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, dev);
+    return (int)e;
 }
 
 int64_t dd_compact_workspace(int64_t n) { return n <= 0 ? 1 : dd::tiles_of(n); }

@@ -161,11 +161,14 @@ EXPORTS = {
     "dd_abi_version": (ctypes.c_int, []),
     "dd_build_info": (ctypes.c_char_p, []),
     "dd_selftest_sqrt": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "dd_stamp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dd_wall_clock_khz": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
 }
 
 #: symbols a timing-only lab build (tools/build_variants.sh) or an older
 #: committed source built for an A/B run may lack
-_LAB_OPTIONAL = ("dd_build_info", "dd_selftest_sqrt", "dd_rollout_kernel", "dd_device_errors")
+_LAB_OPTIONAL = ("dd_build_info", "dd_selftest_sqrt", "dd_rollout_kernel", "dd_device_errors", "dd_stamp",
+                 "dd_wall_clock_khz")
 
 
 class NativeLibraryError(RuntimeError):

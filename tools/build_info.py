@@ -5,6 +5,7 @@ bodies (step_kernel_isa, rollout_kernel_isa), so a counter summary can be tied
 to the exact code it was measured on (bench.py compares the row's kernel hash
 before reporting roofline.traffic / rollout_point.traffic)."""
 import hashlib
+import re
 import sys
 
 
@@ -18,11 +19,16 @@ def digest(path: str) -> str:
     return h.hexdigest()[:16]
 
 
+_LABEL_NO = re.compile(rb"\.(LBB|LCPI|Lfunc_end|Ltmp)\d+")
+
+
 def kernel_digest(path: str, prefix: bytes) -> str:
     """sha256 of the bodies of every function whose symbol starts with
     `prefix` (from its `sym:` label to its `.Lfunc_end` label), comments
     skipped: a change elsewhere in the translation unit leaves it alone, so
-    a PMC row of one kernel stays valid across edits of the others."""
+    a PMC row of one kernel stays valid across edits of the others.  Label
+    numbers that count the functions before it (.LBB<f>_<b>, .Lfunc_end<f>,
+    .Ltmp<k>, .LCPI<f>_<k>) are normalised for the same reason."""
     h = hashlib.sha256()
     inside = False
     with open(path, "rb") as f:
@@ -32,7 +38,7 @@ def kernel_digest(path: str, prefix: bytes) -> str:
             if inside:
                 if line.lstrip().startswith((b";", b"//")):
                     continue
-                h.update(line)
+                h.update(_LABEL_NO.sub(rb".\1", line))
                 if line.startswith(b".Lfunc_end"):
                     inside = False
     return h.hexdigest()[:16]

@@ -14,10 +14,10 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path[:0] = [REPO, os.path.join(REPO, "reinforcement-learning-101_amd")]
+sys.path[:0] = [REPO, os.path.join(REPO, "reinforcement-learning-101_amd"), os.path.dirname(os.path.abspath(__file__))]
 import torch  # noqa: E402
+from span_events import KernelSpanEvents  # noqa: E402
 
-import bench  # noqa: E402
 from delivery_drone_amd import EnvConfig, VecDroneEnv  # noqa: E402
 
 
@@ -33,7 +33,7 @@ def main():
     rows = torch.randint(0, 8, (8, a.envs), device=dev, dtype=torch.uint8)
     stream = torch.cuda.Stream(dev)
     Ns = [0, 1, 2, 5, 10, 20, 40]
-    spans = {n: bench.KernelSpanEvents() for n in Ns}
+    spans = {n: KernelSpanEvents() for n in Ns}
     graphs = {}
     with torch.cuda.stream(stream):
         for k in range(3):

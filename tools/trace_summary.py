@@ -32,6 +32,7 @@ def main():
     per = {}
     for r in rows:
         d = per.setdefault(int(r["Dispatch_Id"]), {"us": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3,
+                                                   "t0": int(r["Start_Timestamp"]), "t1": int(r["End_Timestamp"]),
                                                    "kernel": r["Kernel_Name"]})
         if "Counter_Name" in r:
             d[r["Counter_Name"]] = float(r["Counter_Value"])
@@ -45,6 +46,10 @@ def main():
            "last": args.last, "us_mean_last": round(statistics.mean(us[-args.last:]), 2),
            "us_median_last": round(statistics.median(us[-args.last:]), 2),
            "us_per_launch": [round(u, 1) for u in us]}
+    if len(ids) > 1:  # idle time between one selected launch's end and the next one's start
+        gaps = [(per[b]["t0"] - per[a]["t1"]) / 1e3 for a, b in zip(ids, ids[1:])]
+        out["gap_us_median"] = round(statistics.median(gaps), 2)
+        out["span_us"] = round((per[ids[-1]]["t1"] - per[ids[0]]["t0"]) / 1e3, 2)
     if ids and "GRBM_GUI_ACTIVE" in per[ids[0]]:
         ghz = [per[i]["GRBM_GUI_ACTIVE"] / 8 / (per[i]["us"] * 1e3) for i in ids]
         out["effective_clock_ghz"] = [round(g, 3) for g in ghz]
