@@ -45,8 +45,17 @@ def main():
     p.add_argument("--reps", type=int, default=15)
     p.add_argument("--rows", type=int, default=8)
     p.add_argument("--methods", default="graph_ev,graph_stamp,graph,direct")
+    p.add_argument("--sched", default="", choices=["", "auto", "spin", "yield"],
+                   help="hipSetDeviceFlags(hipDeviceSchedule*) before the first GPU work (default: leave it)")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
+    if args.sched:
+        torch.cuda.init()
+        events0 = KernelSpanEvents()  # the HIP runtime torch loaded
+        flag = {"auto": 0, "spin": 1, "yield": 2}[args.sched]
+        rc = events0.hip.hipSetDeviceFlags(ctypes.c_uint(flag))
+        print(json.dumps({"sched": args.sched, "hipSetDeviceFlags_rc": rc}), flush=True)
+        events0.close()
     n = args.envs
     cfg = EnvConfig(randomize_drone=True, randomize_platform=True, auto_reset=True, seed=0)
     env = VecDroneEnv(n, device=dev, config=cfg)
@@ -141,7 +150,7 @@ def main():
                         res[m][2].append((span_ms(m) - cal[m]) / k * 1e3)
             for m in methods:
                 w, h, kern = res[m]
-                row = {"envs": n, "k": k, "method": m, "us_per_step_median": round(statistics.median(w), 3),
+                row = {"envs": n, "k": k, "method": m, "sched": args.sched or "default", "us_per_step_median": round(statistics.median(w), 3),
                        "us_per_step_min": round(min(w), 3),
                        "steps_per_s_median": round(n / (statistics.median(w) * 1e-6), 1),
                        "host_submit_us_per_step": round(statistics.median(h), 3)}
