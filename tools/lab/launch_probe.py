@@ -10,6 +10,8 @@ shape (device sync, K steps, device sync; perf_counter around it):
   graph        the same graphs with no markers
   direct       K dd_step calls straight through ctypes (prebuilt argument
                structs, one per action row), no graph
+  ramp:A+B+..  plain graphs of A, then B, ... steps (the last size repeated
+               until K): a small first graph starts the GPU sooner
 
 Prints one JSON line per (K, method): median / min wall us per step over R
 repetitions, the host submission time per step (perf_counter after the last
@@ -101,6 +103,16 @@ def main():
             return graphs[key]
 
         def run(method, k):
+            if method.startswith("ramp:"):  # graphs of the given sizes in turn (the last one repeated to K)
+                sizes = [int(x) for x in method[5:].split("+")]
+                seq, left = [], k
+                while left > 0:
+                    x = min(sizes[min(len(seq), len(sizes) - 1)], left)
+                    seq.append(x)
+                    left -= x
+                for g in [graph(x, None, False, False) for x in seq]:
+                    g.replay()
+                return
             if method.startswith("graph"):
                 mark = {"graph_ev": "ev", "graph_stamp": "stamp"}.get(method)
                 G = min(50, k)
