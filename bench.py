@@ -274,7 +274,7 @@ def time_steps(env, rows, steps, graph_steps, stream, write_obs=True):
     return e0.elapsed_time(e1) / (reps * graph_steps)
 
 
-def hbm_point(n, precision, seed, dev, write_obs, allocs=3, rounds=6):
+def hbm_point(n, precision, seed, dev, write_obs, allocs=3, rounds=6, contiguous_allocs=2):
     """The same step at an HBM-resident batch (state + obs >> 256 MiB MALL):
     the roofline the config-3 batch cannot show because it lives in cache.
 
@@ -285,7 +285,9 @@ def hbm_point(n, precision, seed, dev, write_obs, allocs=3, rounds=6):
     are allocated one after another and timed in interleaved rounds (order
     reversed every round); every allocation's time is reported, in allocation
     order, and the point's value is their median — the placement spread is
-    shown, not picked from."""
+    shown, not picked from.  `contiguous_allocs` more envs with
+    memory="contiguous" (one physically contiguous range each) are timed in
+    the same rounds and reported beside them (`placements.contiguous`)."""
     import statistics
     import torch
     from delivery_drone_amd import EnvConfig, VecDroneEnv, abi
@@ -294,8 +296,9 @@ def hbm_point(n, precision, seed, dev, write_obs, allocs=3, rounds=6):
     stream = torch.cuda.Stream(dev)
     graph_steps = 10
     runs = []
-    for _ in range(max(1, allocs)):
-        env = VecDroneEnv(n, device=dev, config=cfg, precision=precision)
+    for j in range(max(1, allocs) + max(0, contiguous_allocs)):
+        mem = "torch" if j < max(1, allocs) else "contiguous"
+        env = VecDroneEnv(n, device=dev, config=cfg, precision=precision, memory=mem)
         env.reset()
         with torch.cuda.stream(stream):
             for k in range(3):
@@ -318,18 +321,25 @@ def hbm_point(n, precision, seed, dev, write_obs, allocs=3, rounds=6):
                 e1.record(stream)
             torch.cuda.synchronize(dev)
             ts.append(e0.elapsed_time(e1) / (2 * graph_steps))
-    per_alloc = [statistics.median(ts) for _, _, ts in runs]
-    ms = statistics.median(per_alloc)
     bpe = runs[0][0].step_bytes_per_env(abi.DD_ACT_BITMASK, with_obs=write_obs)
+    contig = [statistics.median(ts) for env, _, ts in runs if env.memory == "contiguous"]
+    per_alloc = [statistics.median(ts) for env, _, ts in runs if env.memory == "torch"]
+    ms = statistics.median(per_alloc)
     gbs = bpe * n / (ms * 1e-3) / 1e9
     out = {"envs": n, "us_per_step": round(ms * 1e3, 3), "steps_per_s": round(n / (ms * 1e-3), 1),
            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-           "placements": {"allocations": len(runs), "us_per_step_by_allocation": [round(t * 1e3, 1) for t in per_alloc],
+           "placements": {"allocations": len(per_alloc), "us_per_step_by_allocation": [round(t * 1e3, 1) for t in per_alloc],
                           "frac_by_allocation": [round(bpe * n / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                                  for t in per_alloc],
                           "frac_min": round(bpe * n / (max(per_alloc) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                           "frac_max": round(bpe * n / (min(per_alloc) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                          "value": "median over allocations"},
+                          "value": "median over allocations",
+                          "contiguous": {"allocations": len(contig),
+                                         "us_per_step_by_allocation": [round(t * 1e3, 1) for t in contig],
+                                         "frac_by_allocation": [round(bpe * n / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                                                for t in contig],
+                                         "note": "VecDroneEnv(memory='contiguous'): every field in one "
+                                                 "physically contiguous range, timed in the same rounds"}},
            "traffic": pmc_traffic(n, precision, write_obs), "bytes_per_env": bpe}
     del runs, rows
     torch.cuda.empty_cache()

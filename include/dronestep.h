@@ -455,6 +455,20 @@ int dd_selftest_sqrt(uint64_t seed, int64_t n, unsigned long long *mismatches, v
 int dd_stamp(unsigned long long *slot, void *stream);
 int dd_wall_clock_khz(int *khz);
 
+/* Device memory for an env's arrays (not a reference interface;
+ * VecDroneEnv(memory=...) carves its SoA fields and per-step outputs from
+ * one range).  DD_MEM_DEFAULT: hipMalloc.  DD_MEM_CONTIGUOUS:
+ * hipExtMallocWithFlags(hipDeviceMallocContiguous), one physically
+ * contiguous range: an HBM-resident batch (16.8M drones) steps at the same
+ * speed from every such allocation (within ~1 %) where hipMalloc'd ones vary
+ * ~10 % with the driver's placement, but a cache-resident
+ * batch (262,144 drones) steps ~35 % slower from it (profiles/r06/lab/).
+ * dd_device_free(NULL) is a no-op. */
+#define DD_MEM_DEFAULT 0
+#define DD_MEM_CONTIGUOUS 1
+int dd_device_alloc(void **ptr, uint64_t bytes, int32_t flags);
+int dd_device_free(void *ptr);
+
 #ifdef __cplusplus
 }
 #endif

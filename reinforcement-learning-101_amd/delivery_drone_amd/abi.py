@@ -33,6 +33,7 @@ DD_SHAPED_PPO, DD_SHAPED_REINFORCE = 0, 1
 DD_ROLLOUT_AUTO, DD_ROLLOUT_SINGLE, DD_ROLLOUT_SPLIT_NO_WAIT = 0, 1, 2
 DD_ROLLOUT_FLUSHED, DD_ROLLOUT_HELD, DD_ROLLOUT_SPLIT = 16, 17, 18
 DD_ERR_HANDOVER = 1
+DD_MEM_DEFAULT, DD_MEM_CONTIGUOUS = 0, 1
 
 _D = ctypes.c_double
 _I = ctypes.c_int32
@@ -163,12 +164,14 @@ EXPORTS = {
     "dd_selftest_sqrt": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "dd_stamp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dd_wall_clock_khz": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "dd_device_alloc": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint64, _I]),
+    "dd_device_free": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 #: symbols a timing-only lab build (tools/build_variants.sh) or an older
 #: committed source built for an A/B run may lack
 _LAB_OPTIONAL = ("dd_build_info", "dd_selftest_sqrt", "dd_rollout_kernel", "dd_device_errors", "dd_stamp",
-                 "dd_wall_clock_khz")
+                 "dd_wall_clock_khz", "dd_device_alloc", "dd_device_free")
 
 
 class NativeLibraryError(RuntimeError):

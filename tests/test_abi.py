@@ -228,6 +228,23 @@ def test_byte_model():
     assert lib.dd_compact_workspace(1000) == 4
 
 
+def test_device_alloc_rejects_bad_arguments():
+    """dd_device_alloc / dd_device_free argument checks (no HIP call reached)."""
+    EINVAL = 1  # hipErrorInvalidValue
+    lib = abi.lib()
+    p = ctypes.c_void_p()
+    assert lib.dd_device_alloc(None, 64, abi.DD_MEM_DEFAULT) == EINVAL
+    assert lib.dd_device_alloc(ctypes.byref(p), 0, abi.DD_MEM_CONTIGUOUS) == EINVAL
+    assert lib.dd_device_alloc(ctypes.byref(p), 64, 7) == EINVAL and p.value is None
+    assert lib.dd_device_free(None) == 0
+
+
+def test_memory_option_is_checked_before_the_gpu():
+    from delivery_drone_amd import VecDroneEnv
+    with pytest.raises(ValueError, match="memory"):
+        VecDroneEnv(8, memory="pinned")
+
+
 def test_no_cpu_fallback_without_gpu():
     import torch
     from delivery_drone_amd import VecDroneEnv

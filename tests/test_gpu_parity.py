@@ -582,6 +582,52 @@ def test_ping_pong_equals_in_place(precision, auto, gpu_device):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
 
 
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_contiguous_memory_equals_torch_memory(precision, gpu_device):
+    """VecDroneEnv(memory="contiguous") (every field and output carved from
+    one dd_device_alloc(DD_MEM_CONTIGUOUS) range at 2 MiB boundaries) steps,
+    rolls out and resets to the same bits as the default allocation; the
+    range is freed with the env's last tensor."""
+    from delivery_drone_amd import abi
+    n, k = 70_001, 60
+    cfg = dict(randomize_drone=True, auto_reset=True, seed=5)
+    a = VecDroneEnv(n, device=gpu_device, precision=precision, **cfg)
+    b = VecDroneEnv(n, device=gpu_device, precision=precision, memory="contiguous", **cfg)
+    assert b.memory == "contiguous"
+    ptrs = sorted(getattr(b, f).data_ptr() for f in gd.FLOAT_FIELDS + ("status", "steps", "episode", "obs", "reward"))
+    assert all(p % (2 << 20) == ptrs[0] % (2 << 20) for p in ptrs)  # one range, 2 MiB-aligned offsets
+    assert ptrs[-1] - ptrs[0] < 64 * (2 << 20) + 8 * n * 16
+    a.reset()
+    b.reset()
+    g = torch.Generator(device=gpu_device).manual_seed(6)
+    acts = torch.randint(0, 8, (k, n), device=gpu_device, dtype=torch.uint8, generator=g)
+    for t in range(k):
+        oa, ra, da, _ = a.step(acts[t])
+        ob, rb, db, _ = b.step(acts[t])
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    ra = a.rollout(acts[:16], frames=16)
+    rb = b.rollout(acts[:16], frames=16)
+    for x, y in zip(ra, rb):
+        assert torch.equal(x, y)
+    for f in gd.FLOAT_FIELDS + ("status", "steps", "episode"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert (b.status & gd.ST_DONE).any() or int(b.episode.max()) > 1
+    with pytest.raises(ValueError):
+        VecDroneEnv(16, device=gpu_device, memory="pinned")
+    # the range goes with the last tensor over it
+    free0, _ = torch.cuda.mem_get_info(gpu_device)
+    big = VecDroneEnv(1 << 22, device=gpu_device, memory="contiguous")
+    free1, _ = torch.cuda.mem_get_info(gpu_device)
+    assert free0 - free1 >= (1 << 22) * 60
+    del big
+    import gc
+    gc.collect()
+    torch.cuda.synchronize(gpu_device)
+    free2, _ = torch.cuda.mem_get_info(gpu_device)
+    assert free2 - free1 >= (1 << 22) * 60
+    assert abi.DD_MEM_CONTIGUOUS == 1
+
+
 def test_ping_pong_rejects_aliasing_and_lane_slices(gpu_device):
     from delivery_drone_amd import abi
     env = VecDroneEnv(256, device=gpu_device, ping_pong=True)

@@ -20,6 +20,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PKG = os.path.join(REPO, "reinforcement-learning-101_amd")
+UNITS = ("drone_step", "policy_mlp", "policy_rollout", "render", "device_memory")  # the Makefile's SRCS
 FLAGS = {"policy_mlp": ["-mllvm", "-disable-machine-licm"], "policy_rollout": ["-mllvm", "-disable-machine-licm"]}
 
 
@@ -57,12 +58,12 @@ def main():
                     seen.add(inc)
                     includes(inc, seen)
         return seen
-    units = [u for u in ("drone_step", "policy_mlp", "policy_rollout", "render")
+    units = [u for u in UNITS
              if any(f == u + ".hip" or f in includes(u + ".hip") for f in fnames)]
     if os.environ.get("DD_VARIANT_UNITS"):
         units = [u for u in units if u in os.environ["DD_VARIANT_UNITS"].split(",")]
     objs = []
-    for u in ("drone_step", "policy_mlp", "policy_rollout", "render"):
+    for u in UNITS:
         if u in units:
             o = os.path.join(src, u + ".o")
             subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
