@@ -69,7 +69,7 @@ run_step() {
             done
         done ;;
     sq)
-        bash tools/pmc_sq.sh $OUT ;;
+        bash tools/pmc_sq.sh $TAG/sq > $OUT/sq_step_counters.txt; local rc=$?; cat $OUT/sq_step_counters.txt; return $rc ;;
     roll5)
         # bench.py's rollout_point schedule: 1 + 120 warm launches, then the 40 it times (last 40 of 161)
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_c5 -o roll -f csv -- python3 tools/prof_driver.py \
