@@ -7,6 +7,7 @@ slab (field k at a 2 MiB boundary, tools/lab/diag_alloc.rebind_slab's layout):
   torch   the slab from torch's caching allocator (hipMalloc underneath)
   contig  the slab from hipExtMallocWithFlags(hipDeviceMallocContiguous),
           wrapped for torch through __cuda_array_interface__
+  V:S     variant V with field k at a 2 MiB boundary + k * S bytes
 
 `--allocs A` envs of each variant, allocated alternately; all are timed in
 interleaved rounds (order reversed every other round), graphs of G steps.
@@ -45,12 +46,16 @@ def hip_runtime():
 
 
 def rebind(env, how, hip, keep):
+    """how: "torch" / "contig", optionally ":S" — field k then starts at a
+    2 MiB boundary + k * S bytes (in a contiguous range: a physical stagger)."""
+    how, _, stagger = how.partition(":")
+    stagger = int(stagger or 0)
     names = list(_FLOAT_FIELDS) + ["status", "steps", "episode", "obs", "reward", "_done"]
     tens = [getattr(env, k) for k in names]
     align = 2 << 20
     offs, pos = [], 0
-    for t in tens:
-        pos = (pos + align - 1) // align * align
+    for k, t in enumerate(tens):
+        pos = (pos + align - 1) // align * align + k * stagger
         offs.append(pos)
         pos += t.numel() * t.element_size()
     total = pos + align
