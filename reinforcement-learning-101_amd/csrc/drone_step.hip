@@ -193,15 +193,20 @@ __device__ __forceinline__ void load_raw(const Soa<T>& a, const void* actions, u
 // Everything after the loads for one lane: the frame (or sticky done / auto
 // reset), the state and output stores, the observation row into `orow`
 // (LDS).  Returns whether the lane's episode ended in this call.  The fast
-// frame (kExact false) may report the lane risky (frame.h): then nothing is
-// stored, and the kernel calls finish_lane again with kExact.
+// frame may report the lane risky (frame.h): then, in a wave-uniform rare
+// branch, the lane's frame is redone at once from its loaded inputs with
+// kExact (glibc's sin, cos and pow), and the rest of the lane's work is
+// shared.  (Until round 6 a second finish_lane pass over the risky lanes
+// redid everything after the loads: the same results, but that copy of the
+// observation, reward and store code cost config 3 1-2 % in time and ~110
+// instruction-wait cycles per wave, profiles/r06/lab/step_inline_exact.jsonl.)
 // kShape: the notebooks' reward fused (frame.h, kShapePpo / kShapeReinforce).
 // kPP (ping-pong, DDStepIO.state_out): the nine per-frame fields (x y vx vy
 // angle omega fuel total steps) go to `o`; px, py, status and episode always
 // go to `a`.  In place (the usual case) the kernel has no `o` at all.
-template <typename T, bool kRef, int kShape, bool kPP, bool kExact = false>
+template <typename T, bool kRef, int kShape, bool kPP>
 __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, const Soa<T>& o, uint32_t i,
-                                            const Raw<T>& r, float* orow, bool* risky = nullptr) {
+                                            const Raw<T>& r, float* orow) {
     const DDConfig& sw = p.k.c;
     const Consts& k = kRef ? kRefConsts : p.k;
     Lane s;
@@ -230,11 +235,13 @@ __device__ __forceinline__ bool finish_lane(const StepArgs& p, const Soa<T>& a, 
         }
     } else {
         bool rk = false;
-        reward = frame<kRef, false, kExact>(k, sw, r.act, s, &rk);
-        if constexpr (!kExact) {
-            if (__builtin_expect(rk, 0)) {  // the exact pass redoes this lane: store nothing now
-                *risky = true;
-                return false;
+        reward = frame<kRef, false>(k, sw, r.act, s, &rk);
+        if (__builtin_expect(__ballot(rk) != 0, 0)) {
+            if (rk) {  // the frame again from the loaded state, the reference's functions (frame.h)
+                s.x = r.x; s.y = r.y; s.vx = r.vx; s.vy = r.vy; s.angle = r.angle; s.omega = r.omega;
+                s.fuel = r.fuel; s.px = r.px; s.py = r.py; s.total = r.total; s.status = r.status;
+                s.steps = r.steps;
+                reward = frame<kRef, false, true>(k, sw, r.act, s, nullptr);
             }
         }
         if constexpr (kShape != kShapeNone) {
@@ -300,13 +307,8 @@ __device__ __forceinline__ void step_tile(const StepArgs& p, const Soa<T>& a, co
                  "s"(a.px), "s"(a.py), "s"(a.total), "s"(a.status), "s"(a.steps), "s"(p.actions));
     Raw<T> r;
     if (i < (uint32_t)p.n) load_raw<T, AFMT>(a, p.actions, i, r);
-    bool risky = false;
-    bool ended = i < (uint32_t)p.n &&
-                 finish_lane<T, kRef, kShape, kPP>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM, &risky);
-    if (__builtin_expect(__ballot(risky) != 0, 0)) {  // the rare exact pass (frame.h): glibc's sin, cos and pow
-        if (risky)
-            ended = finish_lane<T, kRef, kShape, kPP, true>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM);
-    }
+    const bool ended = i < (uint32_t)p.n &&
+                       finish_lane<T, kRef, kShape, kPP>(p, a, o, i, r, tile + threadIdx.x * DD_OBS_DIM);
     if (p.done_idx) {  // wave-ballot compaction of the lanes that just ended
         const uint64_t m = __ballot(ended);
         if (m) {
